@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""Benchmark: forward-model SS evaluations/sec on the 299-cell TestData (BASELINE.json metric).
+
+One *step* = one batched ssfun launch over the whole per-GPU workload: every TestData cell
+(299) x P DRAM-style proposals (default 256), i.e. the evaluations mcmcstat would request
+from 299 independent chains over P lockstep proposals. Proposals are Gaussian around the
+fixture chain states with the reference's proposal variances J0 (TranscriptionCycleMCMC.m:
+217-231); proposals outside the parameter box (:242-255) are marked inactive and are NOT
+counted (mcmcstat rejects them without calling ssfun). All inputs are resident in HBM before
+timing; the kernel is launched on torch's current stream through the C ABI.
+
+Multi-GPU (torchrun, one process per GPU, RCCL): weak scaling -- every rank evaluates its own
+replica of the 299-cell workload with a rank-specific seed; there is no data-path collective.
+The per-cell results are gathered once after timing (the reference's parfor output assembly),
+and the elapsed time is the max over ranks.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+CONSTRUCT = "P2P-MS2v5-LacZ-PP7v4"
+
+
+def proposal_batch(cells, P: int, seed: int):
+    """theta (B, ld), cell_id (B,), active (B,) for 299 cells x P proposals."""
+    from transcriptioncycleinference_amd.data import DR_BOUNDS, LOWER, UPPER
+
+    z = np.load(os.path.join(ROOT, "tests", "golden", "chain_theta.npz"), allow_pickle=False)
+    off = z["theta_offsets"]
+    rng = np.random.default_rng(seed)
+    C = cells.n_cells
+    lens = cells.lengths
+    ld = int(7 + lens.max())
+    B = C * P
+    theta = np.zeros((B, ld))
+    cid = np.repeat(np.arange(C, dtype=np.int32), P)
+    # current chain state per cell: a random fixture row of that cell
+    rows_of = [np.nonzero(z["cell_id"] == c)[0] for c in range(C)]
+    for c in range(C):
+        n = int(lens[c])
+        t = cells.cell(c)[0]
+        picks = rng.choice(rows_of[c], P)
+        st = np.stack([z["theta"][off[i]:off[i + 1]] for i in picks])
+        # proposal variances J0 = diag([v 0.05, tau 0.1, ton dt_last, MS2 1, PP7 1, A 0.05, R 0.5, dR 0.5])
+        var = np.concatenate([[0.05, 0.1, t[-1] - t[-2], 1.0, 1.0, 0.05, 0.5], np.full(n, 0.5)])
+        theta[c * P:(c + 1) * P, :7 + n] = st + rng.normal(0.0, 1.0, st.shape) * np.sqrt(var)
+    core = theta[:, :7]
+    active = np.all((core >= LOWER) & (core <= UPPER), axis=1)
+    for c in range(C):
+        n = int(lens[c])
+        dR = theta[c * P:(c + 1) * P, 7:7 + n]
+        active[c * P:(c + 1) * P] &= np.all((dR >= DR_BOUNDS[0]) & (dR <= DR_BOUNDS[1]), axis=1)
+    return theta, cid, active.astype(np.uint8)
+
+
+def algorithmic_bytes(cells, cid, active) -> int:
+    """per active eval theta 8*(7+N_c) + cell id 4; per row active flag 1 +
+    SS write 8; per launch the cell data t/MS2/PP7 24*N_c once per cell."""
+    lens = cells.lengths.astype(np.int64)
+    act = active.astype(bool)
+    per_active = (8 * (7 + lens[cid[act]]) + 4).sum()
+    return int(per_active + 9 * len(cid) + 24 * lens.sum())
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(cells, theta, cid, active, seconds: float):
+    """The C oracle (faithful matrix-form restatement, OpenMP over rows -- the parfor analogue)
+    on the host cores, on a bounded sample of the same workload."""
+    from oracle import c_oracle, oracle as ref  # cpu_baseline leg only
+
+    c_oracle.build()
+    cs = ref.builtin_construct(CONSTRUCT)
+    threads = c_oracle.max_threads()
+    # sample: every cell, the first proposals of each, enough rows to keep all threads busy
+    P = len(cid) // cells.n_cells
+    per_cell = max(1, min(P, (threads * 8 + cells.n_cells - 1) // cells.n_cells))
+    idx = np.concatenate([np.arange(c * P, c * P + per_cell) for c in range(cells.n_cells)])
+    th, ci, ac = theta[idx], cid[idx], active[idx]
+    n_act = int(ac.sum())
+    evals, t0 = 0, time.perf_counter()
+    reps = 0
+    while True:
+        c_oracle.ss_batch(cells.offsets, cells.t, cells.ms2, cells.pp7, cs, th, ci, ac, nthreads=threads)
+        evals += n_act
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": evals / el, "unit": "SS evals/s", "cores": threads, "kind": "port",
+            "sample": f"{len(idx)} rows ({per_cell} proposals x {cells.n_cells} cells, {n_act} in-bounds) x {reps} "
+                      f"passes = {evals} evals in {el:.1f} s; C matrix-form oracle (oracle/tci_oracle.c), "
+                      f"OpenMP {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--proposals", type=int, default=256, help="DRAM-style proposals per cell per launch")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from transcriptioncycleinference_amd import Likelihood, testdata
+
+    cells = testdata()
+    theta, cid, active = proposal_batch(cells, args.proposals, seed=20201028 + rank)
+    B, ld = theta.shape
+    n_active = int(active.sum())
+    lk = Likelihood(cells, CONSTRUCT, device=local)
+    th_d = torch.from_numpy(theta).to(dev)
+    cid_d = torch.from_numpy(cid).to(dev)
+    act_d = torch.from_numpy(active).to(dev)
+    out_d = torch.empty(B, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = e0.elapsed_time(e1) / args.steps  # per launch, HIP events on the launch stream
+
+    ss = out_d.cpu().numpy()
+    finite_ok = bool(np.all(np.isfinite(ss[active.astype(bool)])))
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        cnt = torch.tensor([n_active], dtype=torch.int64, device=dev)
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+        total_active = int(cnt.item())
+        # the one results collective: per-cell SS of the last proposal of every cell (RCCL)
+        from transcriptioncycleinference_amd.parallel import gather_rows
+
+        per_cell = ss.reshape(cells.n_cells, -1)[:, -1].copy()
+        gathered = gather_rows(per_cell, device=f"cuda:{local}")
+        assert len(gathered) == cells.n_cells * world
+    else:
+        total_active = n_active
+
+    workload = f"TestData-299cells-x{args.proposals}proposals"
+    alg = algorithmic_bytes(cells, cid, active)
+    achieved = alg / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic(workload)
+    res = {
+        "metric": "forward-model SS evals/sec, 299-cell TestData, 200k-step chains @1/2/4/8 GPU",
+        "value": total_active * args.steps / elapsed,
+        "unit": "SS evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "reference TestData.mat (299 cells) + synthetic DRAM-style proposals around the fixture chain states",
+        "config": {
+            "workload": workload,
+            "cells_per_gpu": cells.n_cells,
+            "proposals_per_cell": args.proposals,
+            "rows_per_step_per_gpu": B,
+            "in_bounds_evals_per_step_per_gpu": n_active,
+            "construct": CONSTRUCT,
+            "parallelism": f"replica-per-gpu x{world} (cells independent; 1 RCCL gather after timing)",
+            "kernel_rows_per_lane": lk.info["rows_per_lane"],
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel_ms": kernel_ms,
+            "algorithmic_bytes_per_launch": alg,
+            "note": "FP64-VALU/latency-bound path; HBM fraction reported as the north star asks (DESIGN.md)",
+        },
+        "results_finite": finite_ok,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(cells, theta, cid, active, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    lk.close()
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

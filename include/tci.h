@@ -1,0 +1,135 @@
+/*
+ * tci.h -- C ABI of the MI355X-native TranscriptionCycleInference likelihood path.
+ *
+ * Drop-in boundary: mcmcstat's model.ssfun handle, ss = ssfun(theta, data), set at
+ *   /root/reference/src/TranscriptionCycleMCMC.m:186 (closure over `construct`) and :258,
+ *   called by mcmcrun at :273. The handle wraps
+ *   SumofSquaresFunction_TranscriptionCycleMCMC(construct,data,x)
+ *   (/root/reference/src/SumofSquaresFunction_TranscriptionCycleMCMC.m:1-64), which runs
+ *   ConstantElongationSim (src/dependencies/ConstantElongationSim.m:1-67) and
+ *   GetFluorFromPolPos (src/GetFluorFromPolPos.m:1-71).
+ *
+ * The reference's FFI for this path would be a MATLAB MEX gateway; its source is
+ * matlab/tci_mex.cpp and the binding is shown in INTEGRATION.md.
+ *
+ * Conventions: every entry point returns int status (TCI_OK = 0, negative = error) and
+ * never throws; tci_last_error(ctx) gives the message. Plain pointers and sizes only.
+ * A context is bound to one device and is NOT thread-safe (one context per host thread).
+ * Theta layout (TranscriptionCycleMCMC.m:210, SumofSquares...m:35-42):
+ *   theta = [v, tau, ton, MS2_basal, PP7_basal, A, R, dR_1 .. dR_N]   (P = 7 + N doubles)
+ */
+#ifndef TCI_H_
+#define TCI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TCI_OK 0
+#define TCI_EINVAL (-1)  /* bad argument (null pointer, size, construct table) */
+#define TCI_EHIP (-2)    /* HIP runtime error */
+#define TCI_ENOMEM (-3)  /* host or device allocation failed */
+#define TCI_EDIM (-4)    /* grid length != data length: the reference errors at
+                            ConstantElongationSim.m:47 ("Matrix dimensions must agree") */
+#define TCI_ERANGE (-5)  /* cell id out of range, or ld_theta < 7 + N of that cell */
+
+#define TCI_MAX_SEG 4    /* stem-loop segments per dye (GetFluorFromPolPos.m:47 loop) */
+#define TCI_MAX_POINTS 513 /* acquisition points per cell supported by the kernels */
+
+typedef struct tci_ctx tci_ctx;
+
+/* Ragged struct-of-arrays cell table: cell c owns t/ms2/pp7[offsets[c] .. offsets[c+1]).
+ * Replaces the per-cell data struct {xdata = time, ydata = [MS2, PP7]} built at
+ * TranscriptionCycleMCMC.m:163-181 (schema README.md:11-16). NaN = missing sample.
+ * Borrowed for the duration of tci_create only (copied to the device). */
+typedef struct {
+  int64_t n_cells;
+  const int64_t* offsets; /* [n_cells + 1] */
+  const double* t;
+  const double* ms2;
+  const double* pp7;
+} tci_cells;
+
+/* Reporter construct (GetFluorFromPolPos.m:18-30): gene length L = L0 + tau*v (kb) and,
+ * per segment s, the MS2 and PP7 stem-loop start/end (kb) and loop count (fluorval =
+ * loopn/24). Requirements (checked): 1 <= n_seg <= TCI_MAX_SEG, 0 <= start < end. */
+typedef struct {
+  double L0;
+  int32_t n_seg;
+  const double* ms2_start;
+  const double* ms2_end;
+  const double* ms2_loopn;
+  const double* pp7_start;
+  const double* pp7_end;
+  const double* pp7_loopn;
+} tci_construct;
+
+typedef struct {
+  int32_t device;
+  int32_t rows_per_lane;   /* kernel variant selected from the longest cell */
+  int64_t n_cells;
+  int64_t max_points;
+  int64_t device_bytes;    /* resident cell-table bytes in HBM */
+} tci_info;
+
+/* Fill *out with the construct named by `name`; pointers refer to static storage.
+ * Only "P2P-MS2v5-LacZ-PP7v4" is built in (GetFluorFromPolPos.m:18); any other name
+ * returns TCI_EINVAL, as the reference errors on an undefined construct. */
+int tci_construct_by_name(const char* name, tci_construct* out);
+
+/* Create a context on HIP device `device`: validates the cells, builds each cell's
+ * uniform grid t(1):mean(diff(t)):t(end) (SumofSquares...m:29-30, MATLAB colon rule),
+ * interpolation indices/weights and time steps, and uploads everything to HBM. */
+int tci_create(const tci_cells* cells, const tci_construct* construct, int device, tci_ctx** out);
+int tci_destroy(tci_ctx* ctx);
+const char* tci_last_error(const tci_ctx* ctx);
+int tci_get_info(const tci_ctx* ctx, tci_info* out);
+
+/* Test hook: 1 forces the exact sequential loading-counter scan in every evaluation
+ * (normally taken only when the fast parallel scan cannot prove floor() exact). */
+int tci_set_force_exact_scan(tci_ctx* ctx, int enable);
+
+/* Batched likelihood, HOST pointers, synchronous: for b in [0,B)
+ *   ss_out[b] = SumofSquaresFunction_TranscriptionCycleMCMC(construct, cell[cell_id[b]], theta[b,:])
+ * theta is B rows of ld_theta doubles (ld_theta >= 7 + N of the row's cell).
+ * active (may be NULL = all active): rows with active[b] == 0 are skipped (mcmcstat
+ * rejects out-of-bounds proposals without calling ssfun) and get ss_out[b] = +Inf.
+ * Non-finite theta entries give ss_out[b] = NaN (mcmcstat treats it as a rejection). */
+int tci_ss_batch(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int32_t* cell_id,
+                 const uint8_t* active, int64_t B, double* ss_out);
+
+/* Same on DEVICE pointers, asynchronous on `stream` (a hipStream_t; NULL = the context's
+ * own stream). Inputs stay resident in HBM; nothing is copied or synchronised. Rows whose
+ * cell id is out of range or whose ld_theta is too short get NaN. */
+int tci_ss_batch_async(tci_ctx* ctx, const double* d_theta, int64_t ld_theta, const int32_t* d_cell_id,
+                       const uint8_t* d_active, int64_t B, double* d_ss_out, void* stream);
+
+/* One evaluation: the literal ssfun(theta, data) call for one cell (host pointers).
+ * P must be >= 7 + N of the cell. */
+int tci_ssfun(tci_ctx* ctx, int32_t cell, const double* theta, int64_t P, double* ss_out);
+
+#define TCI_GRID_INTERP 0 /* through the uniform grid + interp1, as inside the SS
+                             (SumofSquares...m:28-56) */
+#define TCI_GRID_RAW 1    /* on the raw acquisition times, as the plot/summary call
+                             TranscriptionCycleMCMC.m:307-309 (no grid, no interp1) */
+
+/* Batched forward model, HOST pointers, synchronous: simulated MS2 (already x A) and
+ * PP7 at the acquisition times of each row's cell. Row b writes N(cell) values at
+ * ms2_out[b*ld_out] and pp7_out[b*ld_out] (ld_out >= N of the cell); NaN where the
+ * grid does not cover a time (interp1 out of range). */
+int tci_forward(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int32_t* cell_id, int64_t B,
+                int grid_mode, double* ms2_out, double* pp7_out, int64_t ld_out);
+
+/* Number of acquisition points of a cell, and the grid the SS uses for it (M points). */
+int tci_cell_points(const tci_ctx* ctx, int32_t cell, int64_t* n_out);
+int tci_cell_grid(const tci_ctx* ctx, int32_t cell, double* t_interp_out, int64_t cap, int64_t* m_out);
+
+const char* tci_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TCI_H_ */

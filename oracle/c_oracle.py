@@ -1,0 +1,110 @@
+"""ctypes binding of the C oracle ``oracle/libtci_oracle.so`` (built by ``oracle/Makefile``).
+
+TEST INFRASTRUCTURE ONLY -- importable from ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg; never from the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtci_oracle.so")
+
+_dp = C.POINTER(C.c_double)
+_i64p = C.POINTER(C.c_int64)
+_i32p = C.POINTER(C.c_int32)
+_u8p = C.POINTER(C.c_uint8)
+
+
+class _Construct(C.Structure):
+    _fields_ = [("L0", C.c_double), ("n_seg", C.c_int32),
+                ("ms2_start", _dp), ("ms2_end", _dp), ("ms2_loopn", _dp),
+                ("pp7_start", _dp), ("pp7_end", _dp), ("pp7_loopn", _dp)]
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc, -ffp-contract=off)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.oracle_ss_batch.argtypes = [_i64p, _dp, _dp, _dp, C.c_int64, C.POINTER(_Construct), _dp, C.c_int64,
+                                      _i32p, _u8p, C.c_int64, _dp, _i32p, C.c_int]
+        L.oracle_ss_batch.restype = C.c_int
+        L.oracle_forward.argtypes = [_dp, C.c_int64, C.POINTER(_Construct), _dp, C.c_int, _dp, _dp]
+        L.oracle_forward.restype = C.c_int
+        L.oracle_interp_grid.argtypes = [_dp, C.c_int64, _dp, C.c_int64]
+        L.oracle_interp_grid.restype = C.c_int64
+        L.oracle_max_threads.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _ptr(a, typ):
+    return a.ctypes.data_as(typ) if a is not None else None
+
+
+class _ConstructHolder:
+    def __init__(self, cs):
+        self.arrs = [np.ascontiguousarray(np.asarray(x, np.float64)) for x in
+                     (cs.ms2_start, cs.ms2_end, cs.ms2_loopn, cs.pp7_start, cs.pp7_end, cs.pp7_loopn)]
+        self.s = _Construct(float(cs.L0), len(self.arrs[0]), *[_ptr(a, _dp) for a in self.arrs])
+
+
+def ss_batch(offsets, t, ms2, pp7, construct, theta, cell_id, active=None, nthreads=0):
+    """Batched SS (OpenMP over rows). theta: (B, ld) float64 row-major."""
+    offsets = np.ascontiguousarray(offsets, np.int64)
+    t = np.ascontiguousarray(t, np.float64)
+    ms2 = np.ascontiguousarray(ms2, np.float64)
+    pp7 = np.ascontiguousarray(pp7, np.float64)
+    theta = np.ascontiguousarray(theta, np.float64)
+    cell_id = np.ascontiguousarray(cell_id, np.int32)
+    B, ld = theta.shape
+    act = None if active is None else np.ascontiguousarray(active, np.uint8)
+    out = np.empty(B)
+    st = np.empty(B, np.int32)
+    h = _ConstructHolder(construct)
+    lib().oracle_ss_batch(_ptr(offsets, _i64p), _ptr(t, _dp), _ptr(ms2, _dp), _ptr(pp7, _dp),
+                          len(offsets) - 1, C.byref(h.s), _ptr(theta, _dp), ld, _ptr(cell_id, _i32p),
+                          _ptr(act, _u8p), B, _ptr(out, _dp), _ptr(st, _i32p), int(nthreads))
+    return out, st
+
+
+def forward(t, construct, theta, mode=0):
+    """mode 0: raw times (TranscriptionCycleMCMC.m:307-309); mode 1: grid + interp1."""
+    t = np.ascontiguousarray(t, np.float64)
+    theta = np.ascontiguousarray(theta, np.float64)
+    N = len(t)
+    a = np.empty(N)
+    b = np.empty(N)
+    h = _ConstructHolder(construct)
+    rc = lib().oracle_forward(_ptr(t, _dp), N, C.byref(h.s), _ptr(theta, _dp), int(mode), _ptr(a, _dp), _ptr(b, _dp))
+    if rc != 0:
+        raise RuntimeError(f"oracle_forward failed: {rc}")
+    return a, b
+
+
+def interp_grid(t):
+    t = np.ascontiguousarray(t, np.float64)
+    out = np.empty(len(t) + 8)
+    M = lib().oracle_interp_grid(_ptr(t, _dp), len(t), _ptr(out, _dp), len(out))
+    if M < 0:
+        raise RuntimeError("grid failed")
+    return out[:M]
+
+
+def max_threads() -> int:
+    return int(lib().oracle_max_threads())

@@ -1,0 +1,127 @@
+"""Pin the CPU oracle to the reference's own data before trusting it (CPU only).
+
+Known-answer vectors: ``28-Oct-2020-TestData.mat`` holds ``MCMCplot(c).simMS2/simPP7``, the
+reference's forward model at the posterior means (``TranscriptionCycleMCMC.m:307-309``), for
+all 299 cells. Statistical pin of the full SS (grid + interp1 + nansum): mcmcstat draws
+``1/s2 ~ Gamma(N/2, 2/SS)`` with N = length(ydata) = 2 N_c (``:260``), so over the 2,691
+post-initial chain rows ``s2 * 2N_c / SS(theta)`` must have mean N/(N-2) ~ 1.008 and sd
+sqrt(2/N) ~ 0.091.
+"""
+import numpy as np
+import pytest
+
+from conftest import pack
+from oracle import oracle as O
+
+
+def test_forward_at_means_matches_reference_exactly(cells, means, construct):
+    off = cells.offsets
+    worst = 0.0
+    for c in range(cells.n_cells):
+        t = cells.t[off[c]:off[c + 1]]
+        ms2, pp7 = O.forward_raw(construct, t, means["rows"][c])
+        exp_m = means["sim_ms2"][off[c]:off[c + 1]]
+        exp_p = means["sim_pp7"][off[c]:off[c + 1]]
+        worst = max(worst, np.max(np.abs(ms2 - exp_m) / np.abs(exp_m)), np.max(np.abs(pp7 - exp_p) / np.abs(exp_p)))
+    assert worst <= 1e-12, worst  # observed: 0 (bit-exact)
+
+
+def test_c_oracle_matches_reference_goldens_and_numpy(cells, means, construct, c_oracle):
+    off = cells.offsets
+    for c in range(0, cells.n_cells, 7):
+        t = cells.t[off[c]:off[c + 1]]
+        m, p = c_oracle.forward(t, construct, means["rows"][c], mode=0)
+        np.testing.assert_array_equal(m, means["sim_ms2"][off[c]:off[c + 1]])
+        np.testing.assert_array_equal(p, means["sim_pp7"][off[c]:off[c + 1]])
+        mi, pi = c_oracle.forward(t, construct, means["rows"][c], mode=1)
+        mn, pn = O.forward_interp(construct, t, means["rows"][c])
+        np.testing.assert_array_equal(mi, mn)
+        np.testing.assert_array_equal(pi, pn)
+
+
+def test_grid_length_equals_data_length(cells, c_oracle):
+    """t(1):mean(diff(t)):t(end) has N points ending at t(end) for every TestData cell."""
+    for c in range(cells.n_cells):
+        t = cells.cell(c)[0]
+        g = O.interp_grid(t)
+        assert len(g) == len(t) and g[0] == t[0] and g[-1] == t[-1]
+        np.testing.assert_array_equal(c_oracle.interp_grid(t), g)
+
+
+def test_committed_ss_goldens_reproduce(cells, chain, construct, c_oracle):
+    theta = pack(chain["rows"])
+    ss, st = c_oracle.ss_batch(cells.offsets, cells.t, cells.ms2, cells.pp7, construct, theta, chain["cell_id"])
+    assert np.all(st == 0)
+    np.testing.assert_array_equal(ss, chain["ss"])
+    # numpy restatement on a subset (slow path)
+    for b in range(0, len(theta), 97):
+        c = int(chain["cell_id"][b])
+        assert O.sum_of_squares(construct, cells.data_struct(c), chain["rows"][b]) == chain["ss"][b]
+
+
+def test_s2chain_statistical_pin(cells, chain):
+    lens = cells.lengths
+    post = chain["step"] > 0
+    ratio = chain["s2"][post] * 2 * lens[chain["cell_id"][post]] / chain["ss"][post]
+    assert len(ratio) == 2691
+    n2 = 2 * lens[chain["cell_id"][post]]
+    assert abs(ratio.mean() - np.mean(n2 / (n2 - 2))) < 0.01, ratio.mean()  # 1.0075 observed
+    assert abs(ratio.std() - np.mean(np.sqrt(2 / n2))) < 0.01, ratio.std()  # 0.0911 observed
+
+
+def test_colon_rule_properties():
+    v = O.matlab_colon(0.0, 0.1, 1.0)
+    assert len(v) == 11 and v[-1] == 1.0 and v[0] == 0.0
+    assert len(O.matlab_colon(1.0, 1.0, 5.5)) == 5
+    assert len(O.matlab_colon(2.0, 3.0, 11.0)) == 4
+    assert len(O.matlab_colon(1.0, -1.0, 5.0)) == 0
+    assert np.isnan(O.matlab_colon(0.0, np.nan, 1.0)[0])
+
+
+def test_oracle_quirks(construct):
+    """Semantics the kernels must reproduce."""
+    t = np.linspace(0, 10, 41)
+    th = np.concatenate([[2.0, 1.0, 0.0, 0.0, 0.0, 1.0, 5.0], np.zeros(41)])
+    # dR_N never enters the SS
+    th2 = th.copy()
+    th2[-1] = 29.0
+    d = {"xdata": t, "ydata": np.concatenate([np.ones(41), np.ones(41)])}
+    assert O.sum_of_squares(construct, d, th) == O.sum_of_squares(construct, d, th2)
+    # basal is a floor, not an offset: a huge basal dominates everything
+    th3 = th.copy()
+    th3[3] = 49.0
+    m, _ = O.forward_raw(construct, t, th3)
+    assert np.all(m >= 49.0 * th3[5]) and np.min(m) == 49.0
+    # onset after the last time point: nothing is loaded, signal == floor
+    th4 = th.copy()
+    th4[2] = 10.0
+    m, p = O.forward_raw(construct, t, th4)
+    assert np.all(m == 0) and np.all(p == 0)
+
+
+def test_position_matrix_shape_and_forward_accumulation():
+    """x is m x floor(sum(R.*dt)); loaded columns advance by v*dt(i) per step (ConstantElongationSim.m:47-64)."""
+    t = np.array([0.0, 1.0, 2.0, 3.5])
+    x = O.constant_elongation_sim(1.0, 0.5, np.array([1.5, 1.5, 2.0, -7.0]), t)
+    assert x.shape == (4, 6)  # floor(1.5 + 1.5 + 3.0)
+    # step 1 (t=0 < ton) skipped; step 2 loads floor(1.5)=1; step 3 loads floor(4.5)=4
+    np.testing.assert_array_equal(x[2], [1.0, 0, 0, 0, 0, 0])
+    np.testing.assert_array_equal(x[3], [2.5, 1.5, 1.5, 1.5, 0, 0])
+
+
+@pytest.mark.parametrize("n", [2, 3, 65, 66, 129, 200])
+def test_oracles_agree_on_random_theta(n, construct, c_oracle):
+    rng = np.random.default_rng(n)
+    from transcriptioncycleinference_amd.data import draw_x0, synthetic_times
+
+    t = synthetic_times(rng, n)
+    y1 = rng.normal(3, 2, n)
+    y2 = rng.normal(6, 3, n)
+    y1[rng.random(n) < 0.3] = np.nan
+    off = np.array([0, n])
+    rows = [draw_x0(rng, n) for _ in range(6)]
+    ss, st = c_oracle.ss_batch(off, t, y1, y2, construct, pack(rows), np.zeros(6, np.int32))
+    assert np.all(st == 0)
+    d = {"xdata": t, "ydata": np.concatenate([y1, y2])}
+    for i, r in enumerate(rows):
+        assert ss[i] == O.sum_of_squares(construct, d, r)

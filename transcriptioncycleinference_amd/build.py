@@ -1,0 +1,50 @@
+"""In-tree build of ``libtci.so`` for gfx950 (hipcc; no JIT cache, the .so travels with the repo).
+
+``-ffp-contract=off`` is load-bearing: the loading counter (``counter + R(i)*dt(i)``) and the
+position updates (``x(i,k) + v*dt(i)``) feed floor() and strict comparisons, and MATLAB never
+fuses a multiply into an add. FMA is used only where written explicitly (continuous sums).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_ROOT = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+SOURCES = [os.path.join(CSRC, "tci_kernels.hip"), os.path.join(CSRC, "tci_api.cpp")]
+HEADERS = [os.path.join(REPO_ROOT, "include", "tci.h"), os.path.join(CSRC, "tci_internal.h")]
+LIB = os.path.join(PKG_DIR, "libtci.so")
+ARCH = os.environ.get("TCI_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libtci.so)")
+
+
+def needs_rebuild() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(s) > t for s in SOURCES + HEADERS + [__file__])
+
+
+def build_library(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_rebuild():
+        return LIB
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+           "-Wall", "-I" + os.path.join(REPO_ROOT, "include"), "-I" + CSRC, *SOURCES, "-o", LIB + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build_library(force="--force" in sys.argv, verbose=True))

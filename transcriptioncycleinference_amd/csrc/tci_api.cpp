@@ -1,0 +1,443 @@
+// tci_api.cpp -- C ABI (include/tci.h): context, resident cell table, validation, launches.
+//
+// The context replaces the per-call work the reference repeats inside every ssfun call
+// (SumofSquaresFunction_TranscriptionCycleMCMC.m:28-30: the grid, which is theta-independent)
+// with a one-time build at tci_create, and keeps the cell table resident in HBM.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "tci_internal.h"
+
+using tci::CellMeta;
+using tci::KParams;
+
+struct tci_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int rpl = 1;
+  int64_t n_cells = 0;
+  int64_t max_points = 0;
+  int64_t device_bytes = 0;
+  std::vector<CellMeta> meta;       // host copy
+  std::vector<double> grid;         // host copy of t_interp (packed like the device arrays)
+  KParams kp{};
+  void* dbuf = nullptr;             // one allocation for the whole resident cell table
+  // staging buffers for the host-pointer entry points
+  double* d_theta = nullptr;
+  int32_t* d_cell = nullptr;
+  uint8_t* d_active = nullptr;
+  double* d_out0 = nullptr;
+  double* d_out1 = nullptr;
+  size_t cap_theta = 0, cap_cell = 0, cap_active = 0, cap_out0 = 0, cap_out1 = 0;
+  std::string err;
+};
+
+namespace {
+
+const char kVersion[] = "tci-mi355x 0.1.0 (gfx950)";
+
+int fail(tci_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+int hip_fail(tci_ctx* ctx, hipError_t e, const char* what) {
+  return fail(ctx, TCI_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define TCI_HIP(ctx, call)                                  \
+  do {                                                      \
+    hipError_t e_ = (call);                                 \
+    if (e_ != hipSuccess) return hip_fail((ctx), e_, #call); \
+  } while (0)
+
+double round_half_away(double x) { return x >= 0 ? std::floor(x + 0.5) : -std::floor(-x + 0.5); }
+
+// MATLAB a:d:b by the documented colon algorithm (colonop): n from round((b-a)/d) with a
+// 2*eps*max(|a|,|b|) tolerance, right end snapped to b, and the vector built symmetrically
+// from both ends. Used for t_interp = t(1):dt:t(end) (SumofSquares...m:30).
+std::vector<double> colon(double a, double d, double b) {
+  if (!std::isfinite(a) || !std::isfinite(d) || !std::isfinite(b)) return {NAN};
+  if (d == 0 || (a < b && d < 0) || (b < a && d > 0)) return {};
+  const double tol = 2.0 * 2.220446049250313e-16 * std::max(std::fabs(a), std::fabs(b));
+  const double sig = d > 0 ? 1.0 : -1.0;
+  double n;
+  if (a == std::floor(a) && d == 1) {
+    n = std::floor(b) - a;
+  } else if (a == std::floor(a) && d == std::floor(d)) {
+    const double q = std::floor(a / d);
+    const double r = a - q * d;
+    n = std::floor((b - r) / d) - q;
+  } else {
+    n = round_half_away((b - a) / d);
+    if (sig * (a + n * d - b) > tol) n = n - 1;
+  }
+  if (!(n >= 0) || n > 1e7) return {};
+  const int64_t ni = (int64_t)n;
+  double c = a + n * d;
+  if (sig * (c - b) > -tol) c = b;
+  std::vector<double> v((size_t)ni + 1);
+  for (int64_t k = 0; k <= ni / 2; ++k) {
+    const double kd = (double)k;
+    v[(size_t)k] = a + kd * d;
+    v[(size_t)(ni - k)] = c - kd * d;
+  }
+  if (ni % 2 == 0) v[(size_t)(ni / 2)] = (a + c) / 2;
+  return v;
+}
+
+// dt = mean(t(2:end)-t(1:end-1)) (sequential sum / count), then the colon grid.
+std::vector<double> interp_grid(const double* t, int64_t n) {
+  double s = 0.0;
+  for (int64_t i = 0; i + 1 < n; ++i) s = s + (t[i + 1] - t[i]);
+  return colon(t[0], s / (double)(n - 1), t[n - 1]);
+}
+
+template <typename T>
+int ensure(tci_ctx* ctx, T** p, size_t* cap, size_t need) {
+  if (need <= *cap) return TCI_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  size_t n = std::max(need, (size_t)1024);
+  TCI_HIP(ctx, hipMalloc((void**)p, n * sizeof(T)));
+  *cap = n;
+  return TCI_OK;
+}
+
+int check_construct(tci_ctx* ctx, const tci_construct* cs) {
+  if (!cs) return fail(ctx, TCI_EINVAL, "construct is NULL");
+  if (cs->n_seg < 1 || cs->n_seg > TCI_MAX_SEG)
+    return fail(ctx, TCI_EINVAL, "construct n_seg must be in [1, " + std::to_string(TCI_MAX_SEG) + "]");
+  if (!cs->ms2_start || !cs->ms2_end || !cs->ms2_loopn || !cs->pp7_start || !cs->pp7_end || !cs->pp7_loopn)
+    return fail(ctx, TCI_EINVAL, "construct segment arrays must not be NULL");
+  if (!std::isfinite(cs->L0)) return fail(ctx, TCI_EINVAL, "construct L0 must be finite");
+  for (int s = 0; s < cs->n_seg; ++s) {
+    const double vals[6] = {cs->ms2_start[s], cs->ms2_end[s], cs->ms2_loopn[s],
+                            cs->pp7_start[s], cs->pp7_end[s], cs->pp7_loopn[s]};
+    for (double x : vals)
+      if (!std::isfinite(x)) return fail(ctx, TCI_EINVAL, "construct values must be finite");
+    if (!(cs->ms2_start[s] >= 0 && cs->ms2_start[s] < cs->ms2_end[s] && cs->pp7_start[s] >= 0 &&
+          cs->pp7_start[s] < cs->pp7_end[s]))
+      return fail(ctx, TCI_EINVAL, "construct segment " + std::to_string(s) + " needs 0 <= start < end");
+  }
+  return TCI_OK;
+}
+
+void fill_segments(KParams* kp, const tci_construct* cs) {
+  kp->L0 = cs->L0;
+  kp->n_seg = cs->n_seg;
+  double emax = 0.0;
+  for (int s = 0; s < cs->n_seg; ++s) {
+    tci::SegParams m, p;
+    m.a = cs->ms2_start[s];
+    m.e = cs->ms2_end[s];
+    m.phi = cs->ms2_loopn[s] / 24;  // GetFluorFromPolPos.m:48
+    m.k = m.phi / (m.e - m.a);
+    p.a = cs->pp7_start[s];
+    p.e = cs->pp7_end[s];
+    p.phi = cs->pp7_loopn[s] / 24;  // GetFluorFromPolPos.m:60
+    p.k = p.phi / (p.e - p.a);
+    kp->ms2[s] = m;
+    kp->pp7[s] = p;
+    emax = std::max(emax, std::max(m.e, p.e));
+  }
+  kp->emax = emax;
+}
+
+int pick_rpl(int64_t max_points) {
+  const int64_t steps = max_points - 1;
+  for (int r : {1, 2, 4, 8})
+    if (64 * r >= steps) return r;
+  return -1;
+}
+
+int run(tci_ctx* ctx, int mode, const double* theta, int64_t ld, const int32_t* cell, const uint8_t* active,
+        int64_t B, double* out0, double* out1, int64_t ld_out, void* stream) {
+  TCI_HIP(ctx, hipSetDevice(ctx->device));
+  const int rc = tci::launch(ctx->kp, ctx->rpl, mode, theta, ld, cell, active, B, out0, out1, ld_out,
+                             stream ? stream : (void*)ctx->stream);
+  if (rc != TCI_OK) {
+    if (rc == TCI_EHIP) return hip_fail(ctx, hipGetLastError(), "kernel launch");
+    return fail(ctx, rc, "kernel launch rejected");
+  }
+  return TCI_OK;
+}
+
+// Host-side validation of a host-pointer batch (cell ids and row lengths).
+int check_rows(tci_ctx* ctx, int64_t ld, const int32_t* cell, int64_t B) {
+  for (int64_t b = 0; b < B; ++b) {
+    const int32_t c = cell[b];
+    if (c < 0 || c >= ctx->n_cells)
+      return fail(ctx, TCI_ERANGE, "row " + std::to_string(b) + ": cell id " + std::to_string(c) + " out of range");
+    if (ld < 7 + ctx->meta[(size_t)c].n)
+      return fail(ctx, TCI_ERANGE, "row " + std::to_string(b) + ": theta needs " +
+                                       std::to_string(7 + ctx->meta[(size_t)c].n) + " entries (ld_theta=" +
+                                       std::to_string(ld) + ")");
+  }
+  return TCI_OK;
+}
+
+const double kP2P_ms2_start[1] = {0.024};
+const double kP2P_ms2_end[1] = {1.299};
+const double kP2P_ms2_loopn[1] = {24};
+const double kP2P_pp7_start[1] = {4.292};
+const double kP2P_pp7_end[1] = {5.758};
+const double kP2P_pp7_loopn[1] = {24};
+
+}  // namespace
+
+extern "C" {
+
+const char* tci_version(void) { return kVersion; }
+
+int tci_construct_by_name(const char* name, tci_construct* out) {
+  if (!name || !out) return TCI_EINVAL;
+  // GetFluorFromPolPos.m:18-28
+  if (std::strcmp(name, "P2P-MS2v5-LacZ-PP7v4") == 0) {
+    out->L0 = 6.626;
+    out->n_seg = 1;
+    out->ms2_start = kP2P_ms2_start;
+    out->ms2_end = kP2P_ms2_end;
+    out->ms2_loopn = kP2P_ms2_loopn;
+    out->pp7_start = kP2P_pp7_start;
+    out->pp7_end = kP2P_pp7_end;
+    out->pp7_loopn = kP2P_pp7_loopn;
+    return TCI_OK;
+  }
+  return TCI_EINVAL;
+}
+
+const char* tci_last_error(const tci_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int tci_create(const tci_cells* cells, const tci_construct* construct, int device, tci_ctx** out) {
+  if (!out) return TCI_EINVAL;
+  *out = nullptr;
+  tci_ctx* ctx = new (std::nothrow) tci_ctx();
+  if (!ctx) return TCI_ENOMEM;
+  auto bail = [&](int rc) {
+    *out = ctx;  // hand back the context so the caller can read tci_last_error, then destroy it
+    return rc;
+  };
+  if (!cells || !cells->offsets || !cells->t || !cells->ms2 || !cells->pp7 || cells->n_cells <= 0)
+    return bail(fail(ctx, TCI_EINVAL, "cells table is empty or has NULL arrays"));
+  int rc = check_construct(ctx, construct);
+  if (rc != TCI_OK) return bail(rc);
+  ctx->device = device;
+  ctx->n_cells = cells->n_cells;
+
+  // ---- host precompute of the theta-independent per-cell tables
+  const int64_t C = cells->n_cells;
+  ctx->meta.resize((size_t)C);
+  int64_t total = 0;
+  for (int64_t c = 0; c < C; ++c) {
+    const int64_t n = cells->offsets[c + 1] - cells->offsets[c];
+    if (n < 2) return bail(fail(ctx, TCI_EINVAL, "cell " + std::to_string(c) + " has fewer than 2 points"));
+    if (n > TCI_MAX_POINTS)
+      return bail(fail(ctx, TCI_EINVAL, "cell " + std::to_string(c) + " has " + std::to_string(n) +
+                                            " points (max " + std::to_string(TCI_MAX_POINTS) + ")"));
+    ctx->meta[(size_t)c] = CellMeta{total, (int32_t)n, 0};
+    total += (n + 1) & ~int64_t(1);
+    ctx->max_points = std::max(ctx->max_points, n);
+  }
+  std::vector<double> T((size_t)total, 0.0), Y1((size_t)total, NAN), Y2((size_t)total, NAN), TI((size_t)total, 0.0),
+      DT((size_t)total, 0.0), DTR((size_t)total, 0.0), IW((size_t)total, 0.0);
+  std::vector<int32_t> IK((size_t)total, -1);
+  for (int64_t c = 0; c < C; ++c) {
+    const int64_t o = cells->offsets[c], n = ctx->meta[(size_t)c].n, base = ctx->meta[(size_t)c].base;
+    const double* t = cells->t + o;
+    for (int64_t j = 0; j < n; ++j) {
+      if (!std::isfinite(t[j]))
+        return bail(fail(ctx, TCI_EINVAL, "cell " + std::to_string(c) + ": non-finite time"));
+      if (j > 0 && !(t[j] > t[j - 1]))
+        return bail(fail(ctx, TCI_EINVAL, "cell " + std::to_string(c) + ": times must be strictly increasing"));
+    }
+    std::vector<double> g = interp_grid(t, n);  // SumofSquares...m:29-30
+    if ((int64_t)g.size() != n)
+      return bail(fail(ctx, TCI_EDIM, "cell " + std::to_string(c) + ": grid t(1):mean(diff(t)):t(end) has " +
+                                          std::to_string(g.size()) + " points, data has " + std::to_string(n) +
+                                          " (the reference errors: ConstantElongationSim.m:47)"));
+    for (int64_t j = 0; j < n; ++j) {
+      T[(size_t)(base + j)] = t[j];
+      Y1[(size_t)(base + j)] = cells->ms2[o + j];
+      Y2[(size_t)(base + j)] = cells->pp7[o + j];
+      TI[(size_t)(base + j)] = g[(size_t)j];
+    }
+    for (int64_t i = 0; i + 1 < n; ++i) {
+      DT[(size_t)(base + i)] = g[(size_t)i + 1] - g[(size_t)i];  // ConstantElongationSim.m:43-45
+      DTR[(size_t)(base + i)] = t[i + 1] - t[i];
+    }
+    // interp1(t_interp, y, t): interval k = last grid point <= t_j (clamped to n-2);
+    // outside [t_interp(1), t_interp(end)] -> NaN (k = -1).
+    for (int64_t j = 0; j < n; ++j) {
+      const double q = t[j];
+      if (!(q >= g[0] && q <= g[(size_t)n - 1])) continue;
+      int64_t k = (int64_t)(std::upper_bound(g.begin(), g.end(), q) - g.begin()) - 1;
+      k = std::min(std::max(k, (int64_t)0), n - 2);
+      IK[(size_t)(base + j)] = (int32_t)k;
+      IW[(size_t)(base + j)] = (q - g[(size_t)k]) / (g[(size_t)k + 1] - g[(size_t)k]);
+    }
+  }
+  ctx->grid = TI;
+  ctx->rpl = pick_rpl(ctx->max_points);
+
+  // ---- upload: one resident allocation, 256-byte aligned sub-arrays
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t szD = al((size_t)total * sizeof(double)), szI = al((size_t)total * sizeof(int32_t)),
+               szM = al((size_t)C * sizeof(CellMeta));
+  const size_t bytes = szM + 7 * szD + szI;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipSetDevice"));
+  e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamCreate"));
+  e = hipMalloc(&ctx->dbuf, bytes);
+  if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipMalloc(cell table)"));
+  ctx->device_bytes = (int64_t)bytes;
+  char* p = (char*)ctx->dbuf;
+  auto put = [&](const void* src, size_t n, size_t span) -> void* {
+    void* dst = p;
+    p += span;
+    if (hipMemcpy(dst, src, n, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return dst;
+  };
+  KParams& kp = ctx->kp;
+  const size_t nD = (size_t)total * sizeof(double);
+  kp.cells = (const CellMeta*)put(ctx->meta.data(), (size_t)C * sizeof(CellMeta), szM);
+  kp.T = (const double*)put(T.data(), nD, szD);
+  kp.Y1 = (const double*)put(Y1.data(), nD, szD);
+  kp.Y2 = (const double*)put(Y2.data(), nD, szD);
+  kp.TI = (const double*)put(TI.data(), nD, szD);
+  kp.DT = (const double*)put(DT.data(), nD, szD);
+  kp.DTraw = (const double*)put(DTR.data(), nD, szD);
+  kp.IW = (const double*)put(IW.data(), nD, szD);
+  kp.IK = (const int32_t*)put(IK.data(), (size_t)total * sizeof(int32_t), szI);
+  if (!kp.cells || !kp.T || !kp.Y1 || !kp.Y2 || !kp.TI || !kp.DT || !kp.DTraw || !kp.IW || !kp.IK)
+    return bail(fail(ctx, TCI_EHIP, "hipMemcpy(cell table) failed"));
+  kp.n_cells = C;
+  kp.force_exact = 0;
+  fill_segments(&kp, construct);
+  *out = ctx;
+  return TCI_OK;
+}
+
+int tci_destroy(tci_ctx* ctx) {
+  if (!ctx) return TCI_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (void* q : {(void*)ctx->dbuf, (void*)ctx->d_theta, (void*)ctx->d_cell, (void*)ctx->d_active,
+                  (void*)ctx->d_out0, (void*)ctx->d_out1})
+    if (q) (void)hipFree(q);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return TCI_OK;
+}
+
+int tci_get_info(const tci_ctx* ctx, tci_info* out) {
+  if (!ctx || !out) return TCI_EINVAL;
+  out->device = ctx->device;
+  out->rows_per_lane = ctx->rpl;
+  out->n_cells = ctx->n_cells;
+  out->max_points = ctx->max_points;
+  out->device_bytes = ctx->device_bytes;
+  return TCI_OK;
+}
+
+int tci_set_force_exact_scan(tci_ctx* ctx, int enable) {
+  if (!ctx) return TCI_EINVAL;
+  ctx->kp.force_exact = enable ? 1 : 0;
+  return TCI_OK;
+}
+
+int tci_ss_batch_async(tci_ctx* ctx, const double* d_theta, int64_t ld_theta, const int32_t* d_cell_id,
+                       const uint8_t* d_active, int64_t B, double* d_ss_out, void* stream) {
+  if (!ctx) return TCI_EINVAL;
+  if (B < 0 || (B > 0 && (!d_theta || !d_cell_id || !d_ss_out)))
+    return fail(ctx, TCI_EINVAL, "null device pointer or negative batch");
+  return run(ctx, tci::MODE_SS, d_theta, ld_theta, d_cell_id, d_active, B, d_ss_out, nullptr, 0, stream);
+}
+
+int tci_ss_batch(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int32_t* cell_id,
+                 const uint8_t* active, int64_t B, double* ss_out) {
+  if (!ctx) return TCI_EINVAL;
+  if (B < 0 || (B > 0 && (!theta || !cell_id || !ss_out)))
+    return fail(ctx, TCI_EINVAL, "null pointer or negative batch");
+  if (B == 0) return TCI_OK;
+  int rc = check_rows(ctx, ld_theta, cell_id, B);
+  if (rc != TCI_OK) return rc;
+  TCI_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t nth = (size_t)B * (size_t)ld_theta;
+  if ((rc = ensure(ctx, &ctx->d_theta, &ctx->cap_theta, nth)) != TCI_OK) return rc;
+  if ((rc = ensure(ctx, &ctx->d_cell, &ctx->cap_cell, (size_t)B)) != TCI_OK) return rc;
+  if ((rc = ensure(ctx, &ctx->d_active, &ctx->cap_active, (size_t)B)) != TCI_OK) return rc;
+  if ((rc = ensure(ctx, &ctx->d_out0, &ctx->cap_out0, (size_t)B)) != TCI_OK) return rc;
+  hipStream_t st = ctx->stream;
+  TCI_HIP(ctx, hipMemcpyAsync(ctx->d_theta, theta, nth * sizeof(double), hipMemcpyHostToDevice, st));
+  TCI_HIP(ctx, hipMemcpyAsync(ctx->d_cell, cell_id, (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice, st));
+  if (active)
+    TCI_HIP(ctx, hipMemcpyAsync(ctx->d_active, active, (size_t)B, hipMemcpyHostToDevice, st));
+  rc = run(ctx, tci::MODE_SS, ctx->d_theta, ld_theta, ctx->d_cell, active ? ctx->d_active : nullptr, B, ctx->d_out0,
+           nullptr, 0, st);
+  if (rc != TCI_OK) return rc;
+  TCI_HIP(ctx, hipMemcpyAsync(ss_out, ctx->d_out0, (size_t)B * sizeof(double), hipMemcpyDeviceToHost, st));
+  TCI_HIP(ctx, hipStreamSynchronize(st));
+  return TCI_OK;
+}
+
+int tci_ssfun(tci_ctx* ctx, int32_t cell, const double* theta, int64_t P, double* ss_out) {
+  if (!ctx) return TCI_EINVAL;
+  return tci_ss_batch(ctx, theta, P, &cell, nullptr, 1, ss_out);
+}
+
+int tci_forward(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int32_t* cell_id, int64_t B,
+                int grid_mode, double* ms2_out, double* pp7_out, int64_t ld_out) {
+  if (!ctx) return TCI_EINVAL;
+  if (grid_mode != TCI_GRID_INTERP && grid_mode != TCI_GRID_RAW)
+    return fail(ctx, TCI_EINVAL, "grid_mode must be TCI_GRID_INTERP or TCI_GRID_RAW");
+  if (B < 0 || (B > 0 && (!theta || !cell_id || !ms2_out || !pp7_out)))
+    return fail(ctx, TCI_EINVAL, "null pointer or negative batch");
+  if (B == 0) return TCI_OK;
+  int rc = check_rows(ctx, ld_theta, cell_id, B);
+  if (rc != TCI_OK) return rc;
+  for (int64_t b = 0; b < B; ++b)
+    if (ld_out < ctx->meta[(size_t)cell_id[b]].n) return fail(ctx, TCI_ERANGE, "ld_out shorter than a cell");
+  TCI_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t nth = (size_t)B * (size_t)ld_theta, nout = (size_t)B * (size_t)ld_out;
+  if ((rc = ensure(ctx, &ctx->d_theta, &ctx->cap_theta, nth)) != TCI_OK) return rc;
+  if ((rc = ensure(ctx, &ctx->d_cell, &ctx->cap_cell, (size_t)B)) != TCI_OK) return rc;
+  if ((rc = ensure(ctx, &ctx->d_out0, &ctx->cap_out0, nout)) != TCI_OK) return rc;
+  if ((rc = ensure(ctx, &ctx->d_out1, &ctx->cap_out1, nout)) != TCI_OK) return rc;
+  hipStream_t st = ctx->stream;
+  TCI_HIP(ctx, hipMemcpyAsync(ctx->d_theta, theta, nth * sizeof(double), hipMemcpyHostToDevice, st));
+  TCI_HIP(ctx, hipMemcpyAsync(ctx->d_cell, cell_id, (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice, st));
+  rc = run(ctx, grid_mode == TCI_GRID_RAW ? tci::MODE_FWD_RAW : tci::MODE_FWD_INTERP, ctx->d_theta, ld_theta,
+           ctx->d_cell, nullptr, B, ctx->d_out0, ctx->d_out1, ld_out, st);
+  if (rc != TCI_OK) return rc;
+  TCI_HIP(ctx, hipMemcpyAsync(ms2_out, ctx->d_out0, nout * sizeof(double), hipMemcpyDeviceToHost, st));
+  TCI_HIP(ctx, hipMemcpyAsync(pp7_out, ctx->d_out1, nout * sizeof(double), hipMemcpyDeviceToHost, st));
+  TCI_HIP(ctx, hipStreamSynchronize(st));
+  return TCI_OK;
+}
+
+int tci_cell_points(const tci_ctx* ctx, int32_t cell, int64_t* n_out) {
+  if (!ctx || !n_out || cell < 0 || cell >= ctx->n_cells) return TCI_EINVAL;
+  *n_out = ctx->meta[(size_t)cell].n;
+  return TCI_OK;
+}
+
+int tci_cell_grid(const tci_ctx* ctx, int32_t cell, double* t_interp_out, int64_t cap, int64_t* m_out) {
+  if (!ctx || cell < 0 || cell >= ctx->n_cells) return TCI_EINVAL;
+  const CellMeta& m = ctx->meta[(size_t)cell];
+  if (m_out) *m_out = m.n;
+  if (!t_interp_out) return TCI_OK;
+  if (cap < m.n) return TCI_ERANGE;
+  std::memcpy(t_interp_out, ctx->grid.data() + m.base, (size_t)m.n * sizeof(double));
+  return TCI_OK;
+}
+
+}  // extern "C"

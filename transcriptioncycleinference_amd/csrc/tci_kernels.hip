@@ -1,0 +1,366 @@
+// tci_kernels.hip -- batched FP64 likelihood kernel for gfx950 (CDNA4).
+//
+// One wavefront (64 lanes) evaluates one ssfun(theta, cell):
+//   SumofSquaresFunction_TranscriptionCycleMCMC.m:1-64
+//     -> ConstantElongationSim.m:1-67 -> GetFluorFromPolPos.m:1-71
+// without ever materialising the reference's time x polymerase matrix.
+//
+// Cohort form. Every polymerase loaded at grid step i (ConstantElongationSim.m:60-64)
+// has the same position at every later row r:  p(r,i) = (..((v*dt_i) + v*dt_{i+1}) + ..)
+// + v*dt_{r-1}, accumulated FORWARD exactly as x(i+1,k) = x(i,k) + v*dt(i) does. The
+// c_i = floor(counter_i) - floor(counter_{i-1}) polymerases of step i form one cohort,
+// so a row's stem-loop sum over polymerases is sum_i c_i * f(p(r,i)).
+//
+// Systolic wave layout. Lane l owns RPL consecutive rows (slots g = RPL*l + q, row g+1).
+// At iteration s slot g holds cohort g-s+1; between iterations every cohort moves one
+// slot to the right (register rename inside a lane, one DPP wave_shr:1 across lanes)
+// and adds v*dt of its new row: each (row, cohort) pair costs ONE forward add, in the
+// reference's order, and the row's accumulators never leave registers. The loop ends
+// when no live cohort (c > 0, inside the grid) is short of the gene end, i.e. after the
+// longest elongation window (~L/(v*dt) steps), not after all rows.
+//
+// Loading counter. counter = counter + R(i)*dt(i) (multiply, then add; no FMA) and
+// floor() are discontinuous. A wave-parallel prefix sum gives each step's counter to
+// within a proven bound (|err| <= ~530 ulp of the sum); floor() is taken from it unless
+// some step lands within 2^-42 relative of an integer, in which case the wave re-runs
+// the exact sequential scan (LDS, lane 0). The result is bit-identical to the serial
+// MATLAB loop in both cases.
+//
+// Discontinuous decisions (floor, the strict < / > masks) are computed from values that
+// are bit-identical to the reference's; this file is compiled with -ffp-contract=off so
+// hipcc never fuses them. Continuous parts (row sums, interp1, the residual sum) use
+// explicit FMA / wave reductions and differ from MATLAB only at the ulp level.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "tci_internal.h"
+
+namespace tci {
+
+namespace {
+
+constexpr int kWavesPerBlock = 4;
+
+// DPP wave_shr:1 (GFX9 family; dpp_ctrl 0x138): lane l receives lane l-1, lane 0 gets 0.
+__device__ __forceinline__ double wave_shr1(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x138, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x138, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Order LDS traffic between lanes of ONE wavefront (LDS ops of a wave execute in order;
+// this only stops the compiler from moving accesses across the point).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+  return x;
+}
+
+// Stem-loop occupancy of one polymerase at position p (GetFluorFromPolPos.m:50-52):
+//   phi                 if e < p < L
+//   (p - a)*phi/(e-a)   if a < p < e      (slope precomputed: ulp-level difference only)
+//   0                   otherwise (strict inequalities: p == e gives 0).
+// p <= a makes (p-a)*k <= 0, so max(.,0) realises the p > a test exactly.
+__device__ __forceinline__ double occupancy(double p, const SegParams& s, double L) {
+  double fr = (p - s.a) * s.k;
+  fr = fr > 0.0 ? fr : 0.0;
+  const double full = (p > s.e && p < L) ? s.phi : 0.0;
+  return p < s.e ? fr : full;
+}
+
+template <int RPL, int NSEG, int MODE>
+__global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
+                                                         int64_t ld, const int32_t* __restrict__ cell_id,
+                                                         const uint8_t* __restrict__ active, int64_t B,
+                                                         double* __restrict__ out0, double* __restrict__ out1,
+                                                         int64_t ld_out) {
+  constexpr int SLOTS = 64 * RPL;  // rows 1..SLOTS (row 0 never holds a polymerase)
+  __shared__ double s_rows[kWavesPerBlock][2][SLOTS + 2];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  if (b >= B) return;
+  double* simM = s_rows[wid][0];
+  double* simP = s_rows[wid][1];
+
+  if (MODE == MODE_SS && active != nullptr && active[b] == 0) {
+    if (lane == 0) out0[b] = INFINITY;  // skipped proposal (bounds-rejected by the caller)
+    return;
+  }
+  const int c = __builtin_amdgcn_readfirstlane(cell_id[b]);
+  const bool cell_ok = c >= 0 && c < kp.n_cells;
+  const CellMeta cm = cell_ok ? kp.cells[c] : CellMeta{0, 0, 0};
+  const int N = cm.n;
+  const int64_t base = cm.base;
+  if (!cell_ok || ld < 7 + N) {
+    if (MODE == MODE_SS) {
+      if (lane == 0) out0[b] = NAN;
+    } else {
+      for (int j = lane; j < N; j += 64) out0[b * ld_out + j] = out1[b * ld_out + j] = NAN;
+    }
+    return;
+  }
+  const int nsteps = N - 1;  // loading steps = rows that can hold polymerases
+  const double* th = theta + b * ld;
+  const double v = th[0], tau = th[1], ton = th[2], b1 = th[3], b2 = th[4], A = th[5], R = th[6];
+  const double* DT = (MODE == MODE_FWD_RAW ? kp.DTraw : kp.DT) + base;
+  const double* TG = (MODE == MODE_FWD_RAW ? kp.T : kp.TI) + base;
+
+  // ---- per-step setup: R_full = R + dR (SumofSquares...m:45); R<0 -> 0 (ConstantElongationSim.m:36)
+  double vd[RPL], prod[RPL];
+  bool fin = isfinite(v) && isfinite(tau) && isfinite(ton) && isfinite(b1) && isfinite(b2) && isfinite(A) &&
+             isfinite(R);
+#pragma unroll
+  for (int q = 0; q < RPL; ++q) {
+    const int g = RPL * lane + q;
+    prod[q] = 0.0;
+    vd[q] = 0.0;
+    if (g < nsteps) {
+      const double dtg = DT[g];
+      const double dr = th[7 + g];
+      fin = fin && isfinite(dr);
+      double rho = R + dr;
+      rho = rho < 0.0 ? 0.0 : rho;
+      prod[q] = (TG[g] < ton) ? 0.0 : rho * dtg;  // skipped steps leave the counter unchanged (:57-58)
+      vd[q] = v * dtg;                              // v*dt(i), rounded once, as MATLAB (:64)
+    }
+  }
+  if (!__all(fin)) {  // outside mcmcstat's finite parameter box: reported as NaN
+    if (MODE == MODE_SS) {
+      if (lane == 0) out0[b] = NAN;
+    } else {
+      for (int j = lane; j < N; j += 64) out0[b * ld_out + j] = out1[b * ld_out + j] = NAN;
+    }
+    return;
+  }
+
+  // ---- loading counter (ConstantElongationSim.m:60-61): fast parallel scan + exactness proof
+  double K[RPL];
+  {
+    double loc[RPL];
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      s = s + prod[q];
+      loc[q] = s;
+    }
+    double incl = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const double o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl = incl + o;
+    }
+    double excl = __shfl_up(incl, 1, 64);
+    if (lane == 0) excl = 0.0;
+    bool amb = false;
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      const double S = excl + loc[q];
+      const double eps = S * 0x1p-42;
+      amb = amb || (floor(S - eps) != floor(S + eps));
+      K[q] = floor(S);
+    }
+    if (kp.force_exact || __any(amb)) {
+      // Exact path: the reference's serial loop, counter = counter + R(i)*dt(i).
+#pragma unroll
+      for (int q = 0; q < RPL; ++q) simM[RPL * lane + q] = prod[q];
+      wave_sync();
+      if (lane == 0) {
+        double counter = 0.0;
+        for (int g = 0; g < nsteps; ++g) {
+          counter = counter + simM[g];
+          simP[g] = floor(counter);
+        }
+      }
+      wave_sync();
+#pragma unroll
+      for (int q = 0; q < RPL; ++q) {
+        const int g = RPL * lane + q;
+        K[q] = g < nsteps ? simP[g] : 0.0;
+      }
+      wave_sync();
+    }
+  }
+  double cnt[RPL];
+  {
+    const double kprev = wave_shr1(K[RPL - 1]);
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      const int g = RPL * lane + q;
+      const double km1 = q == 0 ? kprev : K[q - 1];
+      cnt[q] = g < nsteps ? K[q] - km1 : 0.0;  // cohort size c_g
+    }
+  }
+
+  // ---- systolic cohort sweep (positions: ConstantElongationSim.m:64; maps: GetFluorFromPolPos.m:47-66)
+  SegParams sm[NSEG], sp[NSEG];
+#pragma unroll
+  for (int k = 0; k < NSEG; ++k) {
+    sm[k] = kp.ms2[k];
+    sp[k] = kp.pp7[k];
+  }
+  const double L = kp.L0 + tau * v;  // L_MS2 = L_PP7 (GetFluorFromPolPos.m:19-20), no FMA
+  const double pstop = L > kp.emax ? L : kp.emax;  // f(p) == 0 for every p >= pstop
+  double p[RPL], cc[RPL], accM[NSEG][RPL], accP[NSEG][RPL];
+#pragma unroll
+  for (int q = 0; q < RPL; ++q) {
+    p[q] = 0.0;
+    cc[q] = cnt[q];
+#pragma unroll
+    for (int k = 0; k < NSEG; ++k) accM[k][q] = accP[k][q] = 0.0;
+  }
+  // v <= 0: every position stays <= 0 <= loop start, so no polymerase is ever lit.
+  if (v > 0.0) {
+    for (int s = 1; s <= nsteps; ++s) {
+      if (s > 1) {
+        const double pin = wave_shr1(p[RPL - 1]);
+        const double cin = wave_shr1(cc[RPL - 1]);
+#pragma unroll
+        for (int q = RPL - 1; q >= 1; --q) {
+          p[q] = p[q - 1];
+          cc[q] = cc[q - 1];
+        }
+        p[0] = pin;
+        cc[0] = cin;
+      }
+      bool alive = false;
+#pragma unroll
+      for (int q = 0; q < RPL; ++q) {
+        p[q] = p[q] + vd[q];  // x(i+1,k) = x(i,k) + v*dt(i)
+#pragma unroll
+        for (int k = 0; k < NSEG; ++k) {
+          accM[k][q] = fma(cc[q], occupancy(p[q], sm[k], L), accM[k][q]);
+          accP[k][q] = fma(cc[q], occupancy(p[q], sp[k], L), accP[k][q]);
+        }
+        alive = alive | ((cc[q] > 0.0) & (p[q] < pstop) & (RPL * lane + q < nsteps));
+      }
+      if (!__any(alive)) break;
+    }
+  }
+
+  // ---- basal floor inside the segment loop (GetFluorFromPolPos.m:54-57,66-69), x A (SumofSquares...m:51)
+#pragma unroll
+  for (int q = 0; q < RPL; ++q) {
+    const int g = RPL * lane + q;
+    if (g < nsteps) {
+      double m = 0.0, pp = 0.0;
+#pragma unroll
+      for (int k = 0; k < NSEG; ++k) {
+        m = m + accM[k][q];
+        m = m < b1 ? b1 : m;
+        pp = pp + accP[k][q];
+        pp = pp < b2 ? b2 : pp;
+      }
+      simM[g + 1] = A * m;
+      simP[g + 1] = pp;
+    }
+  }
+  if (lane == 0) {  // row 1 of the reference: no polymerase yet
+    double m = 0.0, pp = 0.0;
+#pragma unroll
+    for (int k = 0; k < NSEG; ++k) {
+      m = m < b1 ? b1 : m;
+      pp = pp < b2 ? b2 : pp;
+    }
+    simM[0] = A * m;
+    simP[0] = pp;
+  }
+  wave_sync();
+
+  if (MODE == MODE_FWD_RAW) {
+    for (int j = lane; j < N; j += 64) {
+      out0[b * ld_out + j] = simM[j];
+      out1[b * ld_out + j] = simP[j];
+    }
+    return;
+  }
+
+  // ---- interp1 back to the acquisition times (SumofSquares...m:55-56) and nansum of the
+  //      squared residuals over [MS2, PP7] (:57-64).
+  double ss = 0.0;
+  for (int j = lane; j < N; j += 64) {
+    const int k = kp.IK[base + j];
+    double m = NAN, pp = NAN;
+    if (k >= 0) {
+      const double w = kp.IW[base + j];
+      m = simM[k] + w * (simM[k + 1] - simM[k]);
+      pp = simP[k] + w * (simP[k + 1] - simP[k]);
+    }
+    if (MODE == MODE_FWD_INTERP) {
+      out0[b * ld_out + j] = m;
+      out1[b * ld_out + j] = pp;
+    } else {
+      double r1 = kp.Y1[base + j] - m;
+      r1 = r1 * r1;
+      double r2 = kp.Y2[base + j] - pp;
+      r2 = r2 * r2;
+      if (r1 == r1) ss += r1;  // nansum drops NaN data and NaN simulation alike
+      if (r2 == r2) ss += r2;
+    }
+  }
+  if (MODE == MODE_SS) {
+    ss = wave_sum(ss);
+    if (lane == 0) out0[b] = ss;
+  }
+}
+
+template <int RPL, int NSEG>
+int launch_rpl_seg(const KParams& kp, int mode, const double* theta, int64_t ld, const int32_t* cell_id,
+                   const uint8_t* active, int64_t B, double* out0, double* out1, int64_t ld_out,
+                   hipStream_t stream) {
+  const dim3 block(64 * kWavesPerBlock);
+  const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock));
+  switch (mode) {
+    case MODE_SS:
+      hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE_SS>), grid, block, 0, stream, kp, theta, ld, cell_id,
+                         active, B, out0, out1, ld_out);
+      break;
+    case MODE_FWD_INTERP:
+      hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE_FWD_INTERP>), grid, block, 0, stream, kp, theta, ld,
+                         cell_id, active, B, out0, out1, ld_out);
+      break;
+    case MODE_FWD_RAW:
+      hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE_FWD_RAW>), grid, block, 0, stream, kp, theta, ld,
+                         cell_id, active, B, out0, out1, ld_out);
+      break;
+    default:
+      return TCI_EINVAL;
+  }
+  return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;
+}
+
+template <int RPL>
+int launch_rpl(const KParams& kp, int mode, const double* theta, int64_t ld, const int32_t* cell_id,
+               const uint8_t* active, int64_t B, double* out0, double* out1, int64_t ld_out, hipStream_t stream) {
+  switch (kp.n_seg) {
+    case 1: return launch_rpl_seg<RPL, 1>(kp, mode, theta, ld, cell_id, active, B, out0, out1, ld_out, stream);
+    case 2: return launch_rpl_seg<RPL, 2>(kp, mode, theta, ld, cell_id, active, B, out0, out1, ld_out, stream);
+    case 3: return launch_rpl_seg<RPL, 3>(kp, mode, theta, ld, cell_id, active, B, out0, out1, ld_out, stream);
+    case 4: return launch_rpl_seg<RPL, 4>(kp, mode, theta, ld, cell_id, active, B, out0, out1, ld_out, stream);
+    default: return TCI_EINVAL;
+  }
+}
+
+}  // namespace
+
+int launch(const KParams& kp, int rpl, int mode, const double* theta, int64_t ld_theta, const int32_t* cell_id,
+           const uint8_t* active, int64_t B, double* out0, double* out1, int64_t ld_out, void* stream) {
+  if (B <= 0) return TCI_OK;
+  hipStream_t st = (hipStream_t)stream;
+  switch (rpl) {
+    case 1: return launch_rpl<1>(kp, mode, theta, ld_theta, cell_id, active, B, out0, out1, ld_out, st);
+    case 2: return launch_rpl<2>(kp, mode, theta, ld_theta, cell_id, active, B, out0, out1, ld_out, st);
+    case 4: return launch_rpl<4>(kp, mode, theta, ld_theta, cell_id, active, B, out0, out1, ld_out, st);
+    case 8: return launch_rpl<8>(kp, mode, theta, ld_theta, cell_id, active, B, out0, out1, ld_out, st);
+    default: return TCI_EINVAL;
+  }
+}
+
+}  // namespace tci
