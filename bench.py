@@ -37,7 +37,8 @@ def proposal_batch(cells, P: int, seed: int):
     """theta (B, ld), cell_id (B,), active (B,) for 299 cells x P proposals."""
     from transcriptioncycleinference_amd.data import DR_BOUNDS, LOWER, UPPER
 
-    z = np.load(os.path.join(ROOT, "tests", "golden", "chain_theta.npz"), allow_pickle=False)
+    with np.load(os.path.join(ROOT, "tests", "golden", "chain_theta.npz"), allow_pickle=False) as f:
+        z = {k: f[k] for k in f.files}  # materialise once (NpzFile re-reads on every access)
     off = z["theta_offsets"]
     rng = np.random.default_rng(seed)
     C = cells.n_cells

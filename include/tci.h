@@ -87,9 +87,11 @@ int tci_destroy(tci_ctx* ctx);
 const char* tci_last_error(const tci_ctx* ctx);
 int tci_get_info(const tci_ctx* ctx, tci_info* out);
 
-/* Test hook: 1 forces the exact sequential loading-counter scan in every evaluation
- * (normally taken only when the fast parallel scan cannot prove floor() exact). */
-int tci_set_force_exact_scan(tci_ctx* ctx, int enable);
+/* Test hook. flags bit 0: run the exact sequential loading-counter scan in every evaluation
+ * (normally only when the parallel scan cannot prove floor() exact); bit 1: run the exact
+ * per-(row, cohort) position sweep (normally only when the uniform-grid distance table cannot
+ * prove every stem-loop/gene-end comparison). 0 restores the default. */
+int tci_set_force_exact_scan(tci_ctx* ctx, int flags);
 
 /* Batched likelihood, HOST pointers, synchronous: for b in [0,B)
  *   ss_out[b] = SumofSquaresFunction_TranscriptionCycleMCMC(construct, cell[cell_id[b]], theta[b,:])
@@ -100,9 +102,9 @@ int tci_set_force_exact_scan(tci_ctx* ctx, int enable);
 int tci_ss_batch(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int32_t* cell_id,
                  const uint8_t* active, int64_t B, double* ss_out);
 
-/* Same on DEVICE pointers, asynchronous on `stream` (a hipStream_t; NULL = the context's
- * own stream). Inputs stay resident in HBM; nothing is copied or synchronised. Rows whose
- * cell id is out of range or whose ld_theta is too short get NaN. */
+/* Same on DEVICE pointers, asynchronous on `stream` (a hipStream_t; NULL = the HIP default
+ * stream, as in every HIP API). Inputs stay resident in HBM; nothing is copied or
+ * synchronised. Rows whose cell id is out of range or whose ld_theta is too short get NaN. */
 int tci_ss_batch_async(tci_ctx* ctx, const double* d_theta, int64_t ld_theta, const int32_t* d_cell_id,
                        const uint8_t* d_active, int64_t B, double* d_ss_out, void* stream);
 

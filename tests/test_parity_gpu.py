@@ -118,14 +118,36 @@ def test_wide_parameter_box_vs_oracle(lk, cells, construct, c_oracle):
 
 
 def test_exact_scan_path_is_bitwise_identical(lk, chain):
+    """The parallel counter scan + proof and the serial scan give the same cohorts."""
     theta = pack(chain["rows"])
     fast = lk.ss_batch(theta, chain["cell_id"])
-    lk.set_force_exact_scan(True)
+    lk.set_force_exact(scan=True)
     try:
         exact = lk.ss_batch(theta, chain["cell_id"])
     finally:
-        lk.set_force_exact_scan(False)
+        lk.set_force_exact()
     np.testing.assert_array_equal(fast, exact)
+
+
+def test_exact_position_sweep_vs_distance_table(lk, cells, chain, construct, c_oracle):
+    """The per-(row, cohort) exact sweep and the uniform-grid distance-table convolution agree
+    (ulp-level: the fractional occupancy uses P_m instead of the exact position) and both match
+    the oracle."""
+    from transcriptioncycleinference_amd.data import draw_x0
+
+    rng = np.random.default_rng(5)
+    rows = list(chain["rows"]) + [draw_x0(rng, int(cells.lengths[c])) for c in range(cells.n_cells)]
+    cid = np.concatenate([chain["cell_id"], np.arange(cells.n_cells, dtype=np.int32)])
+    theta = pack(rows)
+    fast = lk.ss_batch(theta, cid)
+    lk.set_force_exact(scan=True, positions=True)
+    try:
+        exact = lk.ss_batch(theta, cid)
+    finally:
+        lk.set_force_exact()
+    want = oracle_ss(c_oracle, cells, construct, theta, cid)
+    assert rel_err(fast, exact) <= 1e-12
+    assert rel_err(exact, want) <= REL and rel_err(fast, want) <= REL
 
 
 def test_integer_counter_forces_exact_fallback(construct, c_oracle):

@@ -38,7 +38,7 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_rebuild():
         return LIB
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wall", "-I" + os.path.join(REPO_ROOT, "include"), "-I" + CSRC, *SOURCES, "-o", LIB + ".tmp"]
+           "-Wall", "-Wno-bitwise-instead-of-logical", "-I" + os.path.join(REPO_ROOT, "include"), "-I" + CSRC, *SOURCES, "-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -93,10 +93,12 @@ std::vector<double> colon(double a, double d, double b) {
 }
 
 // dt = mean(t(2:end)-t(1:end-1)) (sequential sum / count), then the colon grid.
-std::vector<double> interp_grid(const double* t, int64_t n) {
+std::vector<double> interp_grid(const double* t, int64_t n, double* d_out) {
   double s = 0.0;
   for (int64_t i = 0; i + 1 < n; ++i) s = s + (t[i + 1] - t[i]);
-  return colon(t[0], s / (double)(n - 1), t[n - 1]);
+  const double d = s / (double)(n - 1);
+  if (d_out) *d_out = d;
+  return colon(t[0], d, t[n - 1]);
 }
 
 template <typename T>
@@ -161,8 +163,7 @@ int pick_rpl(int64_t max_points) {
 int run(tci_ctx* ctx, int mode, const double* theta, int64_t ld, const int32_t* cell, const uint8_t* active,
         int64_t B, double* out0, double* out1, int64_t ld_out, void* stream) {
   TCI_HIP(ctx, hipSetDevice(ctx->device));
-  const int rc = tci::launch(ctx->kp, ctx->rpl, mode, theta, ld, cell, active, B, out0, out1, ld_out,
-                             stream ? stream : (void*)ctx->stream);
+  const int rc = tci::launch(ctx->kp, ctx->rpl, mode, theta, ld, cell, active, B, out0, out1, ld_out, stream);
   if (rc != TCI_OK) {
     if (rc == TCI_EHIP) return hip_fail(ctx, hipGetLastError(), "kernel launch");
     return fail(ctx, rc, "kernel launch rejected");
@@ -242,7 +243,7 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
     if (n > TCI_MAX_POINTS)
       return bail(fail(ctx, TCI_EINVAL, "cell " + std::to_string(c) + " has " + std::to_string(n) +
                                             " points (max " + std::to_string(TCI_MAX_POINTS) + ")"));
-    ctx->meta[(size_t)c] = CellMeta{total, (int32_t)n, 0};
+    ctx->meta[(size_t)c] = CellMeta{total, (int32_t)n, 0, 0.0, 0.0};
     total += (n + 1) & ~int64_t(1);
     ctx->max_points = std::max(ctx->max_points, n);
   }
@@ -258,7 +259,8 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
       if (j > 0 && !(t[j] > t[j - 1]))
         return bail(fail(ctx, TCI_EINVAL, "cell " + std::to_string(c) + ": times must be strictly increasing"));
     }
-    std::vector<double> g = interp_grid(t, n);  // SumofSquares...m:29-30
+    double dgrid = 0.0;
+    std::vector<double> g = interp_grid(t, n, &dgrid);  // SumofSquares...m:29-30
     if ((int64_t)g.size() != n)
       return bail(fail(ctx, TCI_EDIM, "cell " + std::to_string(c) + ": grid t(1):mean(diff(t)):t(end) has " +
                                           std::to_string(g.size()) + " points, data has " + std::to_string(n) +
@@ -269,10 +271,14 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
       Y2[(size_t)(base + j)] = cells->pp7[o + j];
       TI[(size_t)(base + j)] = g[(size_t)j];
     }
+    double delta = 0.0;
     for (int64_t i = 0; i + 1 < n; ++i) {
       DT[(size_t)(base + i)] = g[(size_t)i + 1] - g[(size_t)i];  // ConstantElongationSim.m:43-45
       DTR[(size_t)(base + i)] = t[i + 1] - t[i];
+      delta = std::max(delta, std::fabs(DT[(size_t)(base + i)] - dgrid));
     }
+    ctx->meta[(size_t)c].d = dgrid;
+    ctx->meta[(size_t)c].delta = delta;
     // interp1(t_interp, y, t): interval k = last grid point <= t_j (clamped to n-2);
     // outside [t_interp(1), t_interp(end)] -> NaN (k = -1).
     for (int64_t j = 0; j < n; ++j) {
@@ -348,9 +354,9 @@ int tci_get_info(const tci_ctx* ctx, tci_info* out) {
   return TCI_OK;
 }
 
-int tci_set_force_exact_scan(tci_ctx* ctx, int enable) {
-  if (!ctx) return TCI_EINVAL;
-  ctx->kp.force_exact = enable ? 1 : 0;
+int tci_set_force_exact_scan(tci_ctx* ctx, int flags) {
+  if (!ctx || flags < 0 || flags > 3) return TCI_EINVAL;
+  ctx->kp.force_exact = flags;
   return TCI_OK;
 }
 
@@ -382,7 +388,7 @@ int tci_ss_batch(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int3
   if (active)
     TCI_HIP(ctx, hipMemcpyAsync(ctx->d_active, active, (size_t)B, hipMemcpyHostToDevice, st));
   rc = run(ctx, tci::MODE_SS, ctx->d_theta, ld_theta, ctx->d_cell, active ? ctx->d_active : nullptr, B, ctx->d_out0,
-           nullptr, 0, st);
+           nullptr, 0, (void*)st);
   if (rc != TCI_OK) return rc;
   TCI_HIP(ctx, hipMemcpyAsync(ss_out, ctx->d_out0, (size_t)B * sizeof(double), hipMemcpyDeviceToHost, st));
   TCI_HIP(ctx, hipStreamSynchronize(st));
@@ -416,7 +422,7 @@ int tci_forward(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int32
   TCI_HIP(ctx, hipMemcpyAsync(ctx->d_theta, theta, nth * sizeof(double), hipMemcpyHostToDevice, st));
   TCI_HIP(ctx, hipMemcpyAsync(ctx->d_cell, cell_id, (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice, st));
   rc = run(ctx, grid_mode == TCI_GRID_RAW ? tci::MODE_FWD_RAW : tci::MODE_FWD_INTERP, ctx->d_theta, ld_theta,
-           ctx->d_cell, nullptr, B, ctx->d_out0, ctx->d_out1, ld_out, st);
+           ctx->d_cell, nullptr, B, ctx->d_out0, ctx->d_out1, ld_out, (void*)st);
   if (rc != TCI_OK) return rc;
   TCI_HIP(ctx, hipMemcpyAsync(ms2_out, ctx->d_out0, nout * sizeof(double), hipMemcpyDeviceToHost, st));
   TCI_HIP(ctx, hipMemcpyAsync(pp7_out, ctx->d_out1, nout * sizeof(double), hipMemcpyDeviceToHost, st));

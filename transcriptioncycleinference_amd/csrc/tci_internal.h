@@ -11,8 +11,10 @@ namespace tci {
 // struct-of-arrays at [base, base + n); base is a multiple of 2 (16-byte aligned rows).
 struct CellMeta {
   int64_t base;
-  int32_t n;    // acquisition points N (= grid points M, checked at create)
+  int32_t n;     // acquisition points N (= grid points M, checked at create)
   int32_t pad;
+  double d;      // grid increment of t(1):d:t(end) (SumofSquares...m:29)
+  double delta;  // max_j |(t_interp(j+1) - t_interp(j)) - d| over the grid (a few ulps)
 };
 
 // One stem-loop segment of one dye (GetFluorFromPolPos.m:21-27,48-52,60-64).
@@ -38,7 +40,8 @@ struct KParams {
   double L0;            // gene length before tau*v (GetFluorFromPolPos.m:19)
   double emax;          // max loop end over all segments and dyes
   int32_t n_seg;
-  int32_t force_exact;  // test hook: always run the exact sequential counter scan
+  int32_t force_exact;  // test hook: bit 0 = always run the exact sequential counter scan,
+                        //            bit 1 = always run the exact per-(row, cohort) position sweep
   SegParams ms2[TCI_MAX_SEG];
   SegParams pp7[TCI_MAX_SEG];
 };

@@ -5,31 +5,41 @@
 //     -> ConstantElongationSim.m:1-67 -> GetFluorFromPolPos.m:1-71
 // without ever materialising the reference's time x polymerase matrix.
 //
-// Cohort form. Every polymerase loaded at grid step i (ConstantElongationSim.m:60-64)
-// has the same position at every later row r:  p(r,i) = (..((v*dt_i) + v*dt_{i+1}) + ..)
-// + v*dt_{r-1}, accumulated FORWARD exactly as x(i+1,k) = x(i,k) + v*dt(i) does. The
-// c_i = floor(counter_i) - floor(counter_{i-1}) polymerases of step i form one cohort,
-// so a row's stem-loop sum over polymerases is sum_i c_i * f(p(r,i)).
+// Cohort form. Every polymerase loaded at grid step i (ConstantElongationSim.m:60-64) has the
+// same position at every later row r:  p(r,i) = (..((v*dt_i) + v*dt_{i+1}) + ..) + v*dt_{r-1},
+// accumulated FORWARD exactly as x(i+1,k) = x(i,k) + v*dt(i) does. The
+// c_i = floor(counter_i) - floor(counter_{i-1}) polymerases of step i form one cohort, so a
+// row's stem-loop sum over polymerases is  sum_i c_i * f(p(r,i))  (GetFluorFromPolPos.m:47-66).
 //
-// Systolic wave layout. Lane l owns RPL consecutive rows (slots g = RPL*l + q, row g+1).
-// At iteration s slot g holds cohort g-s+1; between iterations every cohort moves one
-// slot to the right (register rename inside a lane, one DPP wave_shr:1 across lanes)
-// and adds v*dt of its new row: each (row, cohort) pair costs ONE forward add, in the
-// reference's order, and the row's accumulators never leave registers. The loop ends
-// when no live cohort (c > 0, inside the grid) is short of the gene end, i.e. after the
-// longest elongation window (~L/(v*dt) steps), not after all rows.
+// Lane layout. Lane l owns RPL consecutive rows (slots g = RPL*l + q hold row g+1). Cohort
+// values travel between slots by register rename inside a lane and one DPP wave_shr:1 across
+// lanes, so row accumulators never leave registers.
 //
-// Loading counter. counter = counter + R(i)*dt(i) (multiply, then add; no FMA) and
-// floor() are discontinuous. A wave-parallel prefix sum gives each step's counter to
-// within a proven bound (|err| <= ~530 ulp of the sum); floor() is taken from it unless
-// some step lands within 2^-42 relative of an integer, in which case the wave re-runs
-// the exact sequential scan (LDS, lane 0). The result is bit-identical to the serial
-// MATLAB loop in both cases.
+// Loading counter. counter = counter + R(i)*dt(i) (multiply, then add; no FMA) feeds floor().
+// A wave-parallel prefix sum gives every step's counter within a proven bound (<= ~530 ulp of
+// the sum); floor() is taken from it unless a step lands within 2^-42 (relative) of an integer,
+// in which case the wave runs the reference's serial loop (LDS, lane 0). Bit-identical to the
+// serial MATLAB loop either way.
 //
-// Discontinuous decisions (floor, the strict < / > masks) are computed from values that
-// are bit-identical to the reference's; this file is compiled with -ffp-contract=off so
-// hipcc never fuses them. Continuous parts (row sums, interp1, the residual sum) use
-// explicit FMA / wave reductions and differ from MATLAB only at the ulp level.
+// Positions, fast path (uniform grid). The SS grid is t(1):d:t(end), so every step's v*dt is
+// v*d up to a few ulps (delta = max |dt_j - d| is precomputed per cell). A cohort's position
+// after m steps is then m*v*d within a proven bound eps_m, for EVERY cohort. If no
+// representative position P_m = m*(v*d) lies within eps_m of a decision threshold (loop
+// starts/ends, gene end L: the strict < / > of GetFluorFromPolPos.m:50-51,62-63), every
+// (row, cohort) pair at distance m takes the same branch the reference takes, and the row sums
+// are the convolution  sum_m c_{r-m} * F(m),  F(m) = f(P_m)  -- one FMA per (row, distance,
+// dye). Continuous values (the fractional loop occupancy) differ from the exact positions only
+// at the ulp level.
+//
+// Positions, exact path. Otherwise (an ambiguous distance, the raw non-uniform grid of the
+// plot/summary forward model, or the test hook) the wave runs the systolic sweep: each cohort
+// carries its exactly-accumulated forward position, one add per (row, cohort) pair in the
+// reference's order, and every branch is decided on bit-identical positions.
+//
+// This file is compiled with -ffp-contract=off (see build.py) so hipcc never fuses the
+// multiply-then-add statements that feed floor() and the strict comparisons. Continuous parts
+// (row sums, interp1, the residual sum) use explicit FMA and wave reductions; they differ from
+// MATLAB only at the ulp level.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -39,7 +49,7 @@ namespace tci {
 
 namespace {
 
-constexpr int kWavesPerBlock = 4;
+constexpr double kUnitRoundoff = 0x1p-53;
 
 // DPP wave_shr:1 (GFX9 family; dpp_ctrl 0x138): lane l receives lane l-1, lane 0 gets 0.
 __device__ __forceinline__ double wave_shr1(double x) {
@@ -48,8 +58,8 @@ __device__ __forceinline__ double wave_shr1(double x) {
   return __hiloint2double(hi, lo);
 }
 
-// Order LDS traffic between lanes of ONE wavefront (LDS ops of a wave execute in order;
-// this only stops the compiler from moving accesses across the point).
+// Order LDS traffic between lanes of ONE wavefront (a wave's LDS ops execute in order; this
+// only stops the compiler from moving accesses across the point).
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -74,21 +84,44 @@ __device__ __forceinline__ double occupancy(double p, const SegParams& s, double
   return p < s.e ? fr : full;
 }
 
+// LDS doubles per wave: the F table (2*NSEG rows of SLOTS+2) doubles as scan scratch and as the
+// simulated MS2/PP7 rows (arrays 0 and 1) once the F table is consumed.
+template <int RPL, int NSEG>
+struct Shape {
+  static constexpr int kSlots = 64 * RPL;
+  static constexpr int kStride = kSlots + 2;
+  static constexpr int kArrays = 2 * NSEG;
+  static constexpr int kWaveDoubles = kArrays * kStride;
+  static constexpr int kWaves = kWaveDoubles * 8 * 4 <= 48 * 1024 ? 4 : 1;  // waves per block
+};
+
+template <int MODE>
+__device__ __forceinline__ void write_nan(int lane, int N, int64_t b, double* out0, double* out1, int64_t ld_out) {
+  if (MODE == MODE_SS) {
+    if (lane == 0) out0[b] = NAN;
+  } else {
+    for (int j = lane; j < N; j += 64) out0[b * ld_out + j] = out1[b * ld_out + j] = NAN;
+  }
+}
+
 template <int RPL, int NSEG, int MODE>
 __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
                                                          int64_t ld_out) {
-  constexpr int SLOTS = 64 * RPL;  // rows 1..SLOTS (row 0 never holds a polymerase)
-  __shared__ double s_rows[kWavesPerBlock][2][SLOTS + 2];
+  using S = Shape<RPL, NSEG>;
+  constexpr int WPB = S::kWaves;
+  constexpr int STRIDE = S::kStride;
+  __shared__ double s_lds[WPB][S::kWaveDoubles];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t b = (int64_t)blockIdx.x * WPB + wid;
   if (b >= B) return;
-  double* simM = s_rows[wid][0];
-  double* simP = s_rows[wid][1];
+  double* lds = s_lds[wid];
+  double* simM = lds;           // array 0
+  double* simP = lds + STRIDE;  // array 1
 
   if (MODE == MODE_SS && active != nullptr && active[b] == 0) {
     if (lane == 0) out0[b] = INFINITY;  // skipped proposal (bounds-rejected by the caller)
@@ -96,15 +129,11 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
   }
   const int c = __builtin_amdgcn_readfirstlane(cell_id[b]);
   const bool cell_ok = c >= 0 && c < kp.n_cells;
-  const CellMeta cm = cell_ok ? kp.cells[c] : CellMeta{0, 0, 0};
+  const CellMeta cm = cell_ok ? kp.cells[c] : CellMeta{0, 0, 0, 0.0, 0.0};
   const int N = cm.n;
   const int64_t base = cm.base;
   if (!cell_ok || ld < 7 + N) {
-    if (MODE == MODE_SS) {
-      if (lane == 0) out0[b] = NAN;
-    } else {
-      for (int j = lane; j < N; j += 64) out0[b * ld_out + j] = out1[b * ld_out + j] = NAN;
-    }
+    write_nan<MODE>(lane, N, b, out0, out1, ld_out);
     return;
   }
   const int nsteps = N - 1;  // loading steps = rows that can hold polymerases
@@ -133,11 +162,7 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
     }
   }
   if (!__all(fin)) {  // outside mcmcstat's finite parameter box: reported as NaN
-    if (MODE == MODE_SS) {
-      if (lane == 0) out0[b] = NAN;
-    } else {
-      for (int j = lane; j < N; j += 64) out0[b * ld_out + j] = out1[b * ld_out + j] = NAN;
-    }
+    write_nan<MODE>(lane, N, b, out0, out1, ld_out);
     return;
   }
 
@@ -162,12 +187,12 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
     bool amb = false;
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
-      const double S = excl + loc[q];
-      const double eps = S * 0x1p-42;
-      amb = amb || (floor(S - eps) != floor(S + eps));
-      K[q] = floor(S);
+      const double Sq = excl + loc[q];
+      const double eps = Sq * 0x1p-42;
+      amb = amb | (floor(Sq - eps) != floor(Sq + eps));
+      K[q] = floor(Sq);
     }
-    if (kp.force_exact || __any(amb)) {
+    if ((kp.force_exact & 1) || __any(amb)) {
       // Exact path: the reference's serial loop, counter = counter + R(i)*dt(i).
 #pragma unroll
       for (int q = 0; q < RPL; ++q) simM[RPL * lane + q] = prod[q];
@@ -188,62 +213,116 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
       wave_sync();
     }
   }
-  double cnt[RPL];
+  double cc[RPL];  // cohort sizes, slot g holds cohort g
   {
     const double kprev = wave_shr1(K[RPL - 1]);
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
       const int g = RPL * lane + q;
       const double km1 = q == 0 ? kprev : K[q - 1];
-      cnt[q] = g < nsteps ? K[q] - km1 : 0.0;  // cohort size c_g
+      cc[q] = g < nsteps ? K[q] - km1 : 0.0;
     }
   }
 
-  // ---- systolic cohort sweep (positions: ConstantElongationSim.m:64; maps: GetFluorFromPolPos.m:47-66)
   SegParams sm[NSEG], sp[NSEG];
 #pragma unroll
   for (int k = 0; k < NSEG; ++k) {
     sm[k] = kp.ms2[k];
     sp[k] = kp.pp7[k];
   }
-  const double L = kp.L0 + tau * v;  // L_MS2 = L_PP7 (GetFluorFromPolPos.m:19-20), no FMA
+  const double L = kp.L0 + tau * v;                 // L_MS2 = L_PP7 (GetFluorFromPolPos.m:19-20), no FMA
   const double pstop = L > kp.emax ? L : kp.emax;  // f(p) == 0 for every p >= pstop
-  double p[RPL], cc[RPL], accM[NSEG][RPL], accP[NSEG][RPL];
+  double accM[NSEG][RPL], accP[NSEG][RPL];
 #pragma unroll
-  for (int q = 0; q < RPL; ++q) {
-    p[q] = 0.0;
-    cc[q] = cnt[q];
+  for (int q = 0; q < RPL; ++q)
 #pragma unroll
     for (int k = 0; k < NSEG; ++k) accM[k][q] = accP[k][q] = 0.0;
-  }
+
   // v <= 0: every position stays <= 0 <= loop start, so no polymerase is ever lit.
   if (v > 0.0) {
-    for (int s = 1; s <= nsteps; ++s) {
-      if (s > 1) {
-        const double pin = wave_shr1(p[RPL - 1]);
-        const double cin = wave_shr1(cc[RPL - 1]);
-#pragma unroll
-        for (int q = RPL - 1; q >= 1; --q) {
-          p[q] = p[q - 1];
-          cc[q] = cc[q - 1];
-        }
-        p[0] = pin;
-        cc[0] = cin;
-      }
-      bool alive = false;
+    // ---- distance table F(m) = f(m*v*d) and its exactness proof (uniform grid only)
+    bool conv = MODE != MODE_FWD_RAW && !(kp.force_exact & 2);
+    int W = 0;
+    if (conv) {
+      const double vd0 = v * cm.d;
+      const double vdl = v * cm.delta;
+      const double vdd = v * (cm.d + cm.delta);
+      bool amb = false;
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {
-        p[q] = p[q] + vd[q];  // x(i+1,k) = x(i,k) + v*dt(i)
+        const int g = RPL * lane + q;
+        const double md = (double)(g + 1);
+        const double Pm = md * vd0;
+        // |p(r, r-m) - P_m| <= m*v*delta + (m+3)*u*m*v*(d+delta); doubled for margin
+        const double eps = 2.0 * (md * vdl + (md + 4.0) * kUnitRoundoff * md * vdd);
+        bool near = fabs(Pm - L) <= eps;
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) {
-          accM[k][q] = fma(cc[q], occupancy(p[q], sm[k], L), accM[k][q]);
-          accP[k][q] = fma(cc[q], occupancy(p[q], sp[k], L), accP[k][q]);
+          near = near | (fabs(Pm - sm[k].a) <= eps) | (fabs(Pm - sm[k].e) <= eps) | (fabs(Pm - sp[k].a) <= eps) |
+                 (fabs(Pm - sp[k].e) <= eps);
+          lds[(2 * k) * STRIDE + g] = occupancy(Pm, sm[k], L);
+          lds[(2 * k + 1) * STRIDE + g] = occupancy(Pm, sp[k], L);
         }
-        alive = alive | ((cc[q] > 0.0) & (p[q] < pstop) & (RPL * lane + q < nsteps));
+        const bool valid = g < nsteps;
+        amb = amb | (valid & near);
+        W += __popcll(__ballot(valid & (Pm < pstop)));
       }
-      if (!__any(alive)) break;
+      conv = !__any(amb);
+      wave_sync();
+    }
+    if (conv) {
+      // ---- convolution: row r accumulates c_{r-m} * F(m), m = 1..W (W = elongation window)
+      for (int m = 1; m <= W; ++m) {
+        if (m > 1) {
+          const double cin = wave_shr1(cc[RPL - 1]);
+#pragma unroll
+          for (int q = RPL - 1; q >= 1; --q) cc[q] = cc[q - 1];
+          cc[0] = cin;
+        }
+#pragma unroll
+        for (int k = 0; k < NSEG; ++k) {
+          const double fm = lds[(2 * k) * STRIDE + m - 1];  // uniform address: LDS broadcast
+          const double fp = lds[(2 * k + 1) * STRIDE + m - 1];
+#pragma unroll
+          for (int q = 0; q < RPL; ++q) {
+            accM[k][q] = fma(cc[q], fm, accM[k][q]);
+            accP[k][q] = fma(cc[q], fp, accP[k][q]);
+          }
+        }
+      }
+    } else {
+      // ---- exact systolic sweep: at iteration s slot g holds cohort g-s+1 with its forward position
+      double p[RPL];
+#pragma unroll
+      for (int q = 0; q < RPL; ++q) p[q] = 0.0;
+      for (int s = 1; s <= nsteps; ++s) {
+        if (s > 1) {
+          const double pin = wave_shr1(p[RPL - 1]);
+          const double cin = wave_shr1(cc[RPL - 1]);
+#pragma unroll
+          for (int q = RPL - 1; q >= 1; --q) {
+            p[q] = p[q - 1];
+            cc[q] = cc[q - 1];
+          }
+          p[0] = pin;
+          cc[0] = cin;
+        }
+        bool alive = false;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+          p[q] = p[q] + vd[q];  // x(i+1,k) = x(i,k) + v*dt(i)
+#pragma unroll
+          for (int k = 0; k < NSEG; ++k) {
+            accM[k][q] = fma(cc[q], occupancy(p[q], sm[k], L), accM[k][q]);
+            accP[k][q] = fma(cc[q], occupancy(p[q], sp[k], L), accP[k][q]);
+          }
+          alive = alive | ((cc[q] > 0.0) & (p[q] < pstop) & (RPL * lane + q < nsteps));
+        }
+        if (!__any(alive)) break;
+      }
     }
   }
+  wave_sync();  // every F-table read is done before the rows overwrite arrays 0/1
 
   // ---- basal floor inside the segment loop (GetFluorFromPolPos.m:54-57,66-69), x A (SumofSquares...m:51)
 #pragma unroll
@@ -262,7 +341,7 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
       simP[g + 1] = pp;
     }
   }
-  if (lane == 0) {  // row 1 of the reference: no polymerase yet
+  if (lane == 0) {  // first row of the reference: no polymerase yet
     double m = 0.0, pp = 0.0;
 #pragma unroll
     for (int k = 0; k < NSEG; ++k) {
@@ -311,24 +390,29 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
   }
 }
 
+template <int RPL, int NSEG, int MODE>
+void launch_one(const KParams& kp, const double* theta, int64_t ld, const int32_t* cell_id, const uint8_t* active,
+                int64_t B, double* out0, double* out1, int64_t ld_out, hipStream_t stream) {
+  constexpr int WPB = Shape<RPL, NSEG>::kWaves;
+  const dim3 block(64 * WPB);
+  const dim3 grid((unsigned)((B + WPB - 1) / WPB));
+  hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE>), grid, block, 0, stream, kp, theta, ld, cell_id, active, B,
+                     out0, out1, ld_out);
+}
+
 template <int RPL, int NSEG>
 int launch_rpl_seg(const KParams& kp, int mode, const double* theta, int64_t ld, const int32_t* cell_id,
                    const uint8_t* active, int64_t B, double* out0, double* out1, int64_t ld_out,
                    hipStream_t stream) {
-  const dim3 block(64 * kWavesPerBlock);
-  const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock));
   switch (mode) {
     case MODE_SS:
-      hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE_SS>), grid, block, 0, stream, kp, theta, ld, cell_id,
-                         active, B, out0, out1, ld_out);
+      launch_one<RPL, NSEG, MODE_SS>(kp, theta, ld, cell_id, active, B, out0, out1, ld_out, stream);
       break;
     case MODE_FWD_INTERP:
-      hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE_FWD_INTERP>), grid, block, 0, stream, kp, theta, ld,
-                         cell_id, active, B, out0, out1, ld_out);
+      launch_one<RPL, NSEG, MODE_FWD_INTERP>(kp, theta, ld, cell_id, active, B, out0, out1, ld_out, stream);
       break;
     case MODE_FWD_RAW:
-      hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE_FWD_RAW>), grid, block, 0, stream, kp, theta, ld,
-                         cell_id, active, B, out0, out1, ld_out);
+      launch_one<RPL, NSEG, MODE_FWD_RAW>(kp, theta, ld, cell_id, active, B, out0, out1, ld_out, stream);
       break;
     default:
       return TCI_EINVAL;

@@ -65,8 +65,9 @@ class Likelihood:
         self._check(self._lib.tci_get_info(self._h, C.byref(i)))
         return {k: getattr(i, k) for k, _ in i._fields_}
 
-    def set_force_exact_scan(self, enable: bool):
-        self._check(self._lib.tci_set_force_exact_scan(self._h, int(bool(enable))))
+    def set_force_exact(self, scan: bool = False, positions: bool = False):
+        """Test hook: force the exact serial counter scan and/or the exact position sweep."""
+        self._check(self._lib.tci_set_force_exact_scan(self._h, int(bool(scan)) | (int(bool(positions)) << 1)))
 
     def grid(self, cell: int) -> np.ndarray:
         m = C.c_int64()
@@ -116,8 +117,8 @@ class Likelihood:
     def ss_batch_device(self, theta, cell_id, out, active=None, stream=None) -> None:
         """Launch on device tensors already resident in HBM (torch tensors or raw pointers):
         ``theta`` (B, ld) float64, ``cell_id`` (B,) int32, ``out`` (B,) float64, optional
-        ``active`` (B,) uint8. ``stream``: a torch stream / raw hipStream_t (None = the
-        context's stream). Nothing is synchronised."""
+        ``active`` (B,) uint8. ``stream``: a torch stream / raw hipStream_t (None or 0 = the
+        HIP default stream). Nothing is synchronised."""
         def addr(x):
             if x is None:
                 return None
