@@ -21,11 +21,12 @@ struct tci_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int rpl = 1;
+  int64_t stride = 0;               // records per cell in the resident tables
   int64_t n_cells = 0;
   int64_t max_points = 0;
   int64_t device_bytes = 0;
   std::vector<CellMeta> meta;       // host copy
-  std::vector<double> grid;         // host copy of t_interp (packed like the device arrays)
+  std::vector<double> grid;         // host copy of t_interp (cell c at c * stride)
   KParams kp{};
   void* dbuf = nullptr;             // one allocation for the whole resident cell table
   // staging buffers for the host-pointer entry points
@@ -236,22 +237,24 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
   // ---- host precompute of the theta-independent per-cell tables
   const int64_t C = cells->n_cells;
   ctx->meta.resize((size_t)C);
-  int64_t total = 0;
   for (int64_t c = 0; c < C; ++c) {
     const int64_t n = cells->offsets[c + 1] - cells->offsets[c];
     if (n < 2) return bail(fail(ctx, TCI_EINVAL, "cell " + std::to_string(c) + " has fewer than 2 points"));
     if (n > TCI_MAX_POINTS)
       return bail(fail(ctx, TCI_EINVAL, "cell " + std::to_string(c) + " has " + std::to_string(n) +
                                             " points (max " + std::to_string(TCI_MAX_POINTS) + ")"));
-    ctx->meta[(size_t)c] = CellMeta{total, (int32_t)n, 0, 0.0, 0.0};
-    total += (n + 1) & ~int64_t(1);
+    ctx->meta[(size_t)c] = CellMeta{(int32_t)n, 0, 0.0, 0.0, 0.0};
     ctx->max_points = std::max(ctx->max_points, n);
   }
-  std::vector<double> T((size_t)total, 0.0), Y1((size_t)total, NAN), Y2((size_t)total, NAN), TI((size_t)total, 0.0),
-      DT((size_t)total, 0.0), DTR((size_t)total, 0.0), IW((size_t)total, 0.0);
-  std::vector<int32_t> IK((size_t)total, -1);
+  ctx->rpl = pick_rpl(ctx->max_points);
+  const int64_t stride = 64 * (ctx->rpl + 1);  // records per cell: every slot/point index a wave touches
+  ctx->stride = stride;
+  const size_t total = (size_t)C * (size_t)stride;
+  std::vector<tci::StepRec> steps(total, tci::StepRec{0.0, 0.0}), steps_raw(total, tci::StepRec{0.0, 0.0});
+  std::vector<tci::PointRec> points(total, tci::PointRec{0.0, NAN, NAN, -1.0});
+  ctx->grid.assign(total, 0.0);
   for (int64_t c = 0; c < C; ++c) {
-    const int64_t o = cells->offsets[c], n = ctx->meta[(size_t)c].n, base = ctx->meta[(size_t)c].base;
+    const int64_t o = cells->offsets[c], n = ctx->meta[(size_t)c].n, base = c * stride;
     const double* t = cells->t + o;
     for (int64_t j = 0; j < n; ++j) {
       if (!std::isfinite(t[j]))
@@ -265,39 +268,38 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
       return bail(fail(ctx, TCI_EDIM, "cell " + std::to_string(c) + ": grid t(1):mean(diff(t)):t(end) has " +
                                           std::to_string(g.size()) + " points, data has " + std::to_string(n) +
                                           " (the reference errors: ConstantElongationSim.m:47)"));
-    for (int64_t j = 0; j < n; ++j) {
-      T[(size_t)(base + j)] = t[j];
-      Y1[(size_t)(base + j)] = cells->ms2[o + j];
-      Y2[(size_t)(base + j)] = cells->pp7[o + j];
-      TI[(size_t)(base + j)] = g[(size_t)j];
-    }
     double delta = 0.0;
-    for (int64_t i = 0; i + 1 < n; ++i) {
-      DT[(size_t)(base + i)] = g[(size_t)i + 1] - g[(size_t)i];  // ConstantElongationSim.m:43-45
-      DTR[(size_t)(base + i)] = t[i + 1] - t[i];
-      delta = std::max(delta, std::fabs(DT[(size_t)(base + i)] - dgrid));
+    for (int64_t i = 0; i < n; ++i) {
+      ctx->grid[(size_t)(base + i)] = g[(size_t)i];
+      if (i + 1 < n) {
+        const double dti = g[(size_t)i + 1] - g[(size_t)i];  // ConstantElongationSim.m:43-45
+        steps[(size_t)(base + i)] = tci::StepRec{dti, g[(size_t)i]};
+        steps_raw[(size_t)(base + i)] = tci::StepRec{t[i + 1] - t[i], t[i]};
+        delta = std::max(delta, std::fabs(dti - dgrid));
+      }
     }
     ctx->meta[(size_t)c].d = dgrid;
     ctx->meta[(size_t)c].delta = delta;
     // interp1(t_interp, y, t): interval k = last grid point <= t_j (clamped to n-2);
     // outside [t_interp(1), t_interp(end)] -> NaN (k = -1).
     for (int64_t j = 0; j < n; ++j) {
+      tci::PointRec& pr = points[(size_t)(base + j)];
+      pr.y1 = cells->ms2[o + j];
+      pr.y2 = cells->pp7[o + j];
       const double q = t[j];
       if (!(q >= g[0] && q <= g[(size_t)n - 1])) continue;
       int64_t k = (int64_t)(std::upper_bound(g.begin(), g.end(), q) - g.begin()) - 1;
       k = std::min(std::max(k, (int64_t)0), n - 2);
-      IK[(size_t)(base + j)] = (int32_t)k;
-      IW[(size_t)(base + j)] = (q - g[(size_t)k]) / (g[(size_t)k + 1] - g[(size_t)k]);
+      pr.k = (double)k;
+      pr.w = (q - g[(size_t)k]) / (g[(size_t)k + 1] - g[(size_t)k]);
     }
   }
-  ctx->grid = TI;
-  ctx->rpl = pick_rpl(ctx->max_points);
 
   // ---- upload: one resident allocation, 256-byte aligned sub-arrays
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t szD = al((size_t)total * sizeof(double)), szI = al((size_t)total * sizeof(int32_t)),
-               szM = al((size_t)C * sizeof(CellMeta));
-  const size_t bytes = szM + 7 * szD + szI;
+  const size_t szM = al((size_t)C * sizeof(CellMeta)), szS = al(total * sizeof(tci::StepRec)),
+               szP = al(total * sizeof(tci::PointRec));
+  const size_t bytes = szM + 2 * szS + szP;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipSetDevice"));
   e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
@@ -313,18 +315,13 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
     return dst;
   };
   KParams& kp = ctx->kp;
-  const size_t nD = (size_t)total * sizeof(double);
   kp.cells = (const CellMeta*)put(ctx->meta.data(), (size_t)C * sizeof(CellMeta), szM);
-  kp.T = (const double*)put(T.data(), nD, szD);
-  kp.Y1 = (const double*)put(Y1.data(), nD, szD);
-  kp.Y2 = (const double*)put(Y2.data(), nD, szD);
-  kp.TI = (const double*)put(TI.data(), nD, szD);
-  kp.DT = (const double*)put(DT.data(), nD, szD);
-  kp.DTraw = (const double*)put(DTR.data(), nD, szD);
-  kp.IW = (const double*)put(IW.data(), nD, szD);
-  kp.IK = (const int32_t*)put(IK.data(), (size_t)total * sizeof(int32_t), szI);
-  if (!kp.cells || !kp.T || !kp.Y1 || !kp.Y2 || !kp.TI || !kp.DT || !kp.DTraw || !kp.IW || !kp.IK)
+  kp.steps = (const tci::StepRec*)put(steps.data(), total * sizeof(tci::StepRec), szS);
+  kp.steps_raw = (const tci::StepRec*)put(steps_raw.data(), total * sizeof(tci::StepRec), szS);
+  kp.points = (const tci::PointRec*)put(points.data(), total * sizeof(tci::PointRec), szP);
+  if (!kp.cells || !kp.steps || !kp.steps_raw || !kp.points)
     return bail(fail(ctx, TCI_EHIP, "hipMemcpy(cell table) failed"));
+  kp.cell_stride = stride;
   kp.n_cells = C;
   kp.force_exact = 0;
   fill_segments(&kp, construct);
@@ -442,7 +439,7 @@ int tci_cell_grid(const tci_ctx* ctx, int32_t cell, double* t_interp_out, int64_
   if (m_out) *m_out = m.n;
   if (!t_interp_out) return TCI_OK;
   if (cap < m.n) return TCI_ERANGE;
-  std::memcpy(t_interp_out, ctx->grid.data() + m.base, (size_t)m.n * sizeof(double));
+  std::memcpy(t_interp_out, ctx->grid.data() + (size_t)cell * (size_t)ctx->stride, (size_t)m.n * sizeof(double));
   return TCI_OK;
 }
 

@@ -7,14 +7,30 @@
 
 namespace tci {
 
-// Per-cell record of the resident cell table. All per-cell arrays in HBM are packed
-// struct-of-arrays at [base, base + n); base is a multiple of 2 (16-byte aligned rows).
+// Resident cell table. Every cell owns a fixed-stride block of `cell_stride` records in each
+// record array, so a wave can address all of its cell's data from the cell id alone and issue
+// every load of an evaluation at once (no dependent meta -> data round trip).
 struct CellMeta {
-  int64_t base;
   int32_t n;     // acquisition points N (= grid points M, checked at create)
   int32_t pad;
   double d;      // grid increment of t(1):d:t(end) (SumofSquares...m:29)
   double delta;  // max_j |(t_interp(j+1) - t_interp(j)) - d| over the grid (a few ulps)
+  double pad2;
+};
+
+// Per grid step g: the step length and the step's start time (ConstantElongationSim.m:43-45,57).
+struct StepRec {
+  double dt;
+  double t;
+};
+
+// Per acquisition point j: interp1 weight and interval (as a double; -1 = outside the grid,
+// SumofSquares...m:55-56) and the data (NaN = missing).
+struct PointRec {
+  double w;
+  double y1;  // MS2
+  double y2;  // PP7
+  double k;
 };
 
 // One stem-loop segment of one dye (GetFluorFromPolPos.m:21-27,48-52,60-64).
@@ -28,15 +44,11 @@ struct SegParams {
 // Kernel arguments: device pointers of the resident cell table + the construct.
 struct KParams {
   const CellMeta* cells;
+  const StepRec* steps;      // uniform grid t_interp (SumofSquares...m:30) and its steps
+  const StepRec* steps_raw;  // raw times t and raw steps (forward on raw t, TranscriptionCycleMCMC.m:307)
+  const PointRec* points;
   int64_t n_cells;
-  const double* T;      // acquisition times t
-  const double* Y1;     // MS2 data (NaN = missing)
-  const double* Y2;     // PP7 data
-  const double* TI;     // uniform grid t_interp (SumofSquares...m:30)
-  const double* DT;     // grid steps t_interp(i+1)-t_interp(i), n-1 used, padded with 0
-  const double* DTraw;  // raw steps t(i+1)-t(i) (forward on raw t, TranscriptionCycleMCMC.m:307)
-  const double* IW;     // interp1 weight s_j of acquisition time j inside its grid interval
-  const int32_t* IK;    // interp1 interval index k_j (-1: outside the grid -> NaN)
+  int64_t cell_stride;       // records per cell in steps/steps_raw/points (= 64*(rows_per_lane+1))
   double L0;            // gene length before tau*v (GetFluorFromPolPos.m:19)
   double emax;          // max loop end over all segments and dyes
   int32_t n_seg;

@@ -26,10 +26,13 @@
 // after m steps is then m*v*d within a proven bound eps_m, for EVERY cohort. If no
 // representative position P_m = m*(v*d) lies within eps_m of a decision threshold (loop
 // starts/ends, gene end L: the strict < / > of GetFluorFromPolPos.m:50-51,62-63), every
-// (row, cohort) pair at distance m takes the same branch the reference takes, and the row sums
-// are the convolution  sum_m c_{r-m} * F(m),  F(m) = f(P_m)  -- one FMA per (row, distance,
-// dye). Continuous values (the fractional loop occupancy) differ from the exact positions only
-// at the ulp level.
+// (row, cohort) pair at distance m takes the branch the reference takes, so the occupancy is a
+// function of the distance alone: 0 while P_m <= a, a ramp (P_m - a)*phi/(e - a) while
+// a < P_m < e, phi while e < P_m < L, 0 after. With K_i = floor(counter_i) the exact cumulative
+// number of polymerases loaded through step i, a row's sum over all polymerases is then
+//   phi * (K[r - f_lo] - K[r - f_hi - 1])  +  sum_{m in ramp} (K[r-m] - K[r-m-1]) * F(m)
+// -- O(1 + ramp length) per row instead of one term per polymerase (the reference) or per
+// cohort. The ramp values use P_m instead of each cohort's exact position: ulp-level only.
 //
 // Positions, exact path. Otherwise (an ambiguous distance, the raw non-uniform grid of the
 // plot/summary forward model, or the test hook) the wave runs the systolic sweep: each cohort
@@ -50,11 +53,33 @@ namespace tci {
 namespace {
 
 constexpr double kUnitRoundoff = 0x1p-53;
+constexpr int kWavesPerBlock = 4;
+
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, ROW_MASK, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, ROW_MASK, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
 
 // DPP wave_shr:1 (GFX9 family; dpp_ctrl 0x138): lane l receives lane l-1, lane 0 gets 0.
-__device__ __forceinline__ double wave_shr1(double x) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x138, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x138, 0xF, 0xF, false);
+__device__ __forceinline__ double wave_shr1(double x) { return dpp_f64<0x138, 0xF>(x); }
+
+// Inclusive wave64 prefix sum in registers (DPP row_shr 1/2/4/8 inside 16-lane rows, then
+// row_bcast:15 and row_bcast:31 across rows): no LDS round trips.
+__device__ __forceinline__ double wave_incl_scan(double x) {
+  x = x + dpp_f64<0x111, 0xF>(x);
+  x = x + dpp_f64<0x112, 0xF>(x);
+  x = x + dpp_f64<0x114, 0xF>(x);
+  x = x + dpp_f64<0x118, 0xF>(x);
+  x = x + dpp_f64<0x142, 0xA>(x);
+  x = x + dpp_f64<0x143, 0xC>(x);
+  return x;
+}
+
+__device__ __forceinline__ double lane63(double x) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), 63);
   return __hiloint2double(hi, lo);
 }
 
@@ -66,11 +91,7 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ double wave_sum(double x) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
-  return x;
-}
+__device__ __forceinline__ int count_true(bool p) { return __popcll(__ballot(p)); }
 
 // Stem-loop occupancy of one polymerase at position p (GetFluorFromPolPos.m:50-52):
 //   phi                 if e < p < L
@@ -84,16 +105,29 @@ __device__ __forceinline__ double occupancy(double p, const SegParams& s, double
   return p < s.e ? fr : full;
 }
 
-// LDS doubles per wave: the F table (2*NSEG rows of SLOTS+2) doubles as scan scratch and as the
-// simulated MS2/PP7 rows (arrays 0 and 1) once the F table is consumed.
-template <int RPL, int NSEG>
-struct Shape {
-  static constexpr int kSlots = 64 * RPL;
-  static constexpr int kStride = kSlots + 2;
-  static constexpr int kArrays = 2 * NSEG;
-  static constexpr int kWaveDoubles = kArrays * kStride;
-  static constexpr int kWaves = kWaveDoubles * 8 * 4 <= 48 * 1024 ? 4 : 1;  // waves per block
+// Distance-table regions of one segment of one dye: ramp m in [r_lo, r_hi] (a < P_m < e),
+// full m in [f_lo, f_hi] (e < P_m < L). Empty ranges have lo > hi.
+struct Regions {
+  int r_lo, r_hi, f_lo, f_hi;
 };
+
+// Row sum of one segment of one dye on the fast path (see the header): K table in LDS at
+// Ktab[i] = K_i (K_i = 0 for i < 0).
+__device__ __forceinline__ double row_sum(const double* Ktab, int r, const Regions& rg, const SegParams& s,
+                                          double vd0) {
+  double acc = 0.0;
+  if (rg.f_lo <= rg.f_hi) acc = s.phi * (Ktab[r - rg.f_lo] - Ktab[r - rg.f_hi - 1]);
+  if (rg.r_lo <= rg.r_hi) {
+    double kA = Ktab[r - rg.r_lo];
+    for (int m = rg.r_lo; m <= rg.r_hi; ++m) {
+      const double kB = Ktab[r - m - 1];
+      const double F = ((double)m * vd0 - s.a) * s.k;
+      acc = fma(kA - kB, F, acc);
+      kA = kB;
+    }
+  }
+  return acc;
+}
 
 template <int MODE>
 __device__ __forceinline__ void write_nan(int lane, int N, int64_t b, double* out0, double* out1, int64_t ld_out) {
@@ -110,37 +144,61 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
                                                          int64_t ld_out) {
-  using S = Shape<RPL, NSEG>;
-  constexpr int WPB = S::kWaves;
-  constexpr int STRIDE = S::kStride;
-  __shared__ double s_lds[WPB][S::kWaveDoubles];
+  constexpr int SLOTS = 64 * RPL;      // rows 1..SLOTS (row 0 never holds a polymerase)
+  constexpr int KOFF = SLOTS + 1;      // K table: Ktab[KOFF + i] = K_i, zeros below
+  constexpr int SIMP = SLOTS + 2;      // offset of the PP7 row array
+  constexpr int NPT = RPL + 1;         // acquisition points per lane (N <= 64*RPL + 1)
+  constexpr int WAVE_DOUBLES = 2 * SLOTS + 4;
+  __shared__ double s_lds[kWavesPerBlock][WAVE_DOUBLES];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t b = (int64_t)blockIdx.x * WPB + wid;
+  const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wid;
   if (b >= B) return;
   double* lds = s_lds[wid];
-  double* simM = lds;           // array 0
-  double* simP = lds + STRIDE;  // array 1
+  double* simM = lds;
+  double* simP = lds + SIMP;
 
-  if (MODE == MODE_SS && active != nullptr && active[b] == 0) {
+  // ---- every load of the evaluation is issued here, in one round trip
+  const int c = __builtin_amdgcn_readfirstlane(cell_id[b]);
+  const bool act = MODE != MODE_SS || active == nullptr || active[b] != 0;
+  if (!act) {
     if (lane == 0) out0[b] = INFINITY;  // skipped proposal (bounds-rejected by the caller)
     return;
   }
-  const int c = __builtin_amdgcn_readfirstlane(cell_id[b]);
-  const bool cell_ok = c >= 0 && c < kp.n_cells;
-  const CellMeta cm = cell_ok ? kp.cells[c] : CellMeta{0, 0, 0, 0.0, 0.0};
+  if (c < 0 || c >= kp.n_cells) {
+    write_nan<MODE>(lane, 0, b, out0, out1, ld_out);
+    return;
+  }
+  const int64_t cbase = (int64_t)c * kp.cell_stride;
+  const StepRec* ST = (MODE == MODE_FWD_RAW ? kp.steps_raw : kp.steps) + cbase;
+  const PointRec* PT = kp.points + cbase;
+  const double* th = theta + b * ld;
+  const CellMeta cm = kp.cells[c];
+  const double v = th[0], tau = th[1], ton = th[2], b1 = th[3], b2 = th[4], A = th[5], R = th[6];
+  double dr[RPL];
+  StepRec st[RPL];
+#pragma unroll
+  for (int q = 0; q < RPL; ++q) {
+    const int g = RPL * lane + q;
+    dr[q] = 7 + g < ld ? th[7 + g] : 0.0;  // speculative (N unknown yet), kept inside the row
+    st[q] = ST[g];                          // g < cell_stride
+  }
+  PointRec pt[NPT];
+  if (MODE != MODE_FWD_RAW) {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int j = lane + 64 * k;
+      if (j <= SLOTS) pt[k] = PT[j];
+      else pt[k] = PointRec{0.0, 0.0, 0.0, -1.0};
+    }
+  }
   const int N = cm.n;
-  const int64_t base = cm.base;
-  if (!cell_ok || ld < 7 + N) {
+  if (ld < 7 + N) {
     write_nan<MODE>(lane, N, b, out0, out1, ld_out);
     return;
   }
   const int nsteps = N - 1;  // loading steps = rows that can hold polymerases
-  const double* th = theta + b * ld;
-  const double v = th[0], tau = th[1], ton = th[2], b1 = th[3], b2 = th[4], A = th[5], R = th[6];
-  const double* DT = (MODE == MODE_FWD_RAW ? kp.DTraw : kp.DT) + base;
-  const double* TG = (MODE == MODE_FWD_RAW ? kp.T : kp.TI) + base;
 
   // ---- per-step setup: R_full = R + dR (SumofSquares...m:45); R<0 -> 0 (ConstantElongationSim.m:36)
   double vd[RPL], prod[RPL];
@@ -149,24 +207,19 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
 #pragma unroll
   for (int q = 0; q < RPL; ++q) {
     const int g = RPL * lane + q;
-    prod[q] = 0.0;
-    vd[q] = 0.0;
-    if (g < nsteps) {
-      const double dtg = DT[g];
-      const double dr = th[7 + g];
-      fin = fin && isfinite(dr);
-      double rho = R + dr;
-      rho = rho < 0.0 ? 0.0 : rho;
-      prod[q] = (TG[g] < ton) ? 0.0 : rho * dtg;  // skipped steps leave the counter unchanged (:57-58)
-      vd[q] = v * dtg;                              // v*dt(i), rounded once, as MATLAB (:64)
-    }
+    const bool valid = g < nsteps;
+    fin = fin && (!valid || isfinite(dr[q]));
+    double rho = R + dr[q];
+    rho = rho < 0.0 ? 0.0 : rho;
+    prod[q] = (valid && !(st[q].t < ton)) ? rho * st[q].dt : 0.0;  // skipped steps add nothing (:57-60)
+    vd[q] = valid ? v * st[q].dt : 0.0;                              // v*dt(i), rounded once (:64)
   }
   if (!__all(fin)) {  // outside mcmcstat's finite parameter box: reported as NaN
     write_nan<MODE>(lane, N, b, out0, out1, ld_out);
     return;
   }
 
-  // ---- loading counter (ConstantElongationSim.m:60-61): fast parallel scan + exactness proof
+  // ---- loading counter (ConstantElongationSim.m:60-61): DPP prefix sum + exactness proof
   double K[RPL];
   {
     double loc[RPL];
@@ -176,19 +229,12 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
       s = s + prod[q];
       loc[q] = s;
     }
-    double incl = s;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const double o = __shfl_up(incl, d, 64);
-      if (lane >= d) incl = incl + o;
-    }
-    double excl = __shfl_up(incl, 1, 64);
-    if (lane == 0) excl = 0.0;
+    const double excl = wave_shr1(wave_incl_scan(s));
     bool amb = false;
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
       const double Sq = excl + loc[q];
-      const double eps = Sq * 0x1p-42;
+      const double eps = Sq * 0x1p-42;  // >> the (g + 16) ulp bound between any two summation orders
       amb = amb | (floor(Sq - eps) != floor(Sq + eps));
       K[q] = floor(Sq);
     }
@@ -213,16 +259,6 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
       wave_sync();
     }
   }
-  double cc[RPL];  // cohort sizes, slot g holds cohort g
-  {
-    const double kprev = wave_shr1(K[RPL - 1]);
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-      const int g = RPL * lane + q;
-      const double km1 = q == 0 ? kprev : K[q - 1];
-      cc[q] = g < nsteps ? K[q] - km1 : 0.0;
-    }
-  }
 
   SegParams sm[NSEG], sp[NSEG];
 #pragma unroll
@@ -240,61 +276,80 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
 
   // v <= 0: every position stays <= 0 <= loop start, so no polymerase is ever lit.
   if (v > 0.0) {
-    // ---- distance table F(m) = f(m*v*d) and its exactness proof (uniform grid only)
-    bool conv = MODE != MODE_FWD_RAW && !(kp.force_exact & 2);
-    int W = 0;
-    if (conv) {
-      const double vd0 = v * cm.d;
+    bool fast = MODE != MODE_FWD_RAW && !(kp.force_exact & 2);
+    const double vd0 = v * cm.d;
+    Regions rgM[NSEG], rgP[NSEG];
+    if (fast) {
+      // ---- distance regions and their exactness proof
       const double vdl = v * cm.delta;
       const double vdd = v * (cm.d + cm.delta);
       bool amb = false;
+      int n_lt_L = 0;
+      int nM_le_a[NSEG], nM_lt_e[NSEG], nM_le_e[NSEG], nP_le_a[NSEG], nP_lt_e[NSEG], nP_le_e[NSEG];
+#pragma unroll
+      for (int k = 0; k < NSEG; ++k) nM_le_a[k] = nM_lt_e[k] = nM_le_e[k] = nP_le_a[k] = nP_lt_e[k] = nP_le_e[k] = 0;
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {
         const int g = RPL * lane + q;
+        const bool valid = g < nsteps;
         const double md = (double)(g + 1);
         const double Pm = md * vd0;
         // |p(r, r-m) - P_m| <= m*v*delta + (m+3)*u*m*v*(d+delta); doubled for margin
         const double eps = 2.0 * (md * vdl + (md + 4.0) * kUnitRoundoff * md * vdd);
         bool near = fabs(Pm - L) <= eps;
+        n_lt_L += count_true(valid & (Pm < L));
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) {
           near = near | (fabs(Pm - sm[k].a) <= eps) | (fabs(Pm - sm[k].e) <= eps) | (fabs(Pm - sp[k].a) <= eps) |
                  (fabs(Pm - sp[k].e) <= eps);
-          lds[(2 * k) * STRIDE + g] = occupancy(Pm, sm[k], L);
-          lds[(2 * k + 1) * STRIDE + g] = occupancy(Pm, sp[k], L);
+          nM_le_a[k] += count_true(valid & (Pm <= sm[k].a));
+          nM_lt_e[k] += count_true(valid & (Pm < sm[k].e));
+          nM_le_e[k] += count_true(valid & (Pm <= sm[k].e));
+          nP_le_a[k] += count_true(valid & (Pm <= sp[k].a));
+          nP_lt_e[k] += count_true(valid & (Pm < sp[k].e));
+          nP_le_e[k] += count_true(valid & (Pm <= sp[k].e));
         }
-        const bool valid = g < nsteps;
         amb = amb | (valid & near);
-        W += __popcll(__ballot(valid & (Pm < pstop)));
       }
-      conv = !__any(amb);
-      wave_sync();
-    }
-    if (conv) {
-      // ---- convolution: row r accumulates c_{r-m} * F(m), m = 1..W (W = elongation window)
-      for (int m = 1; m <= W; ++m) {
-        if (m > 1) {
-          const double cin = wave_shr1(cc[RPL - 1]);
+      fast = !__any(amb);
 #pragma unroll
-          for (int q = RPL - 1; q >= 1; --q) cc[q] = cc[q - 1];
-          cc[0] = cin;
-        }
+      for (int k = 0; k < NSEG; ++k) {
+        rgM[k] = Regions{nM_le_a[k] + 1, nM_lt_e[k], nM_le_e[k] + 1, n_lt_L};
+        rgP[k] = Regions{nP_le_a[k] + 1, nP_lt_e[k], nP_le_e[k] + 1, n_lt_L};
+      }
+    }
+    if (fast) {
+      // ---- K table (exact cumulative loaded counts) and O(1 + ramp) row sums
+      double* Ktab = lds + KOFF;
+#pragma unroll
+      for (int q = 0; q < RPL; ++q) {
+        lds[RPL * lane + q] = 0.0;
+        Ktab[RPL * lane + q] = K[q];
+      }
+      if (lane == 0) lds[SLOTS] = 0.0;
+      wave_sync();
+#pragma unroll
+      for (int q = 0; q < RPL; ++q) {
+        const int r = RPL * lane + q + 1;
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) {
-          const double fm = lds[(2 * k) * STRIDE + m - 1];  // uniform address: LDS broadcast
-          const double fp = lds[(2 * k + 1) * STRIDE + m - 1];
-#pragma unroll
-          for (int q = 0; q < RPL; ++q) {
-            accM[k][q] = fma(cc[q], fm, accM[k][q]);
-            accP[k][q] = fma(cc[q], fp, accP[k][q]);
-          }
+          accM[k][q] = row_sum(Ktab, r, rgM[k], sm[k], vd0);
+          accP[k][q] = row_sum(Ktab, r, rgP[k], sp[k], vd0);
         }
       }
     } else {
       // ---- exact systolic sweep: at iteration s slot g holds cohort g-s+1 with its forward position
-      double p[RPL];
+      double cc[RPL], p[RPL];
+      {
+        const double kprev = wave_shr1(K[RPL - 1]);
 #pragma unroll
-      for (int q = 0; q < RPL; ++q) p[q] = 0.0;
+        for (int q = 0; q < RPL; ++q) {
+          const int g = RPL * lane + q;
+          const double km1 = q == 0 ? kprev : K[q - 1];
+          cc[q] = g < nsteps ? K[q] - km1 : 0.0;
+          p[q] = 0.0;
+        }
+      }
       for (int s = 1; s <= nsteps; ++s) {
         if (s > 1) {
           const double pin = wave_shr1(p[RPL - 1]);
@@ -322,7 +377,7 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
       }
     }
   }
-  wave_sync();  // every F-table read is done before the rows overwrite arrays 0/1
+  wave_sync();  // every K-table read is done before the rows overwrite the LDS
 
   // ---- basal floor inside the segment loop (GetFluorFromPolPos.m:54-57,66-69), x A (SumofSquares...m:51)
 #pragma unroll
@@ -364,28 +419,32 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
   // ---- interp1 back to the acquisition times (SumofSquares...m:55-56) and nansum of the
   //      squared residuals over [MS2, PP7] (:57-64).
   double ss = 0.0;
-  for (int j = lane; j < N; j += 64) {
-    const int k = kp.IK[base + j];
-    double m = NAN, pp = NAN;
-    if (k >= 0) {
-      const double w = kp.IW[base + j];
-      m = simM[k] + w * (simM[k + 1] - simM[k]);
-      pp = simP[k] + w * (simP[k + 1] - simP[k]);
-    }
-    if (MODE == MODE_FWD_INTERP) {
-      out0[b * ld_out + j] = m;
-      out1[b * ld_out + j] = pp;
-    } else {
-      double r1 = kp.Y1[base + j] - m;
-      r1 = r1 * r1;
-      double r2 = kp.Y2[base + j] - pp;
-      r2 = r2 * r2;
-      if (r1 == r1) ss += r1;  // nansum drops NaN data and NaN simulation alike
-      if (r2 == r2) ss += r2;
+#pragma unroll
+  for (int kk = 0; kk < NPT; ++kk) {
+    const int j = lane + 64 * kk;
+    if (j < N) {
+      const int k = (int)pt[kk].k;
+      double m = NAN, pp = NAN;
+      if (k >= 0) {
+        const double w = pt[kk].w;
+        m = simM[k] + w * (simM[k + 1] - simM[k]);
+        pp = simP[k] + w * (simP[k + 1] - simP[k]);
+      }
+      if (MODE == MODE_FWD_INTERP) {
+        out0[b * ld_out + j] = m;
+        out1[b * ld_out + j] = pp;
+      } else {
+        double r1 = pt[kk].y1 - m;
+        r1 = r1 * r1;
+        double r2 = pt[kk].y2 - pp;
+        r2 = r2 * r2;
+        if (r1 == r1) ss += r1;  // nansum drops NaN data and NaN simulation alike
+        if (r2 == r2) ss += r2;
+      }
     }
   }
   if (MODE == MODE_SS) {
-    ss = wave_sum(ss);
+    ss = lane63(wave_incl_scan(ss));
     if (lane == 0) out0[b] = ss;
   }
 }
@@ -393,9 +452,8 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
 template <int RPL, int NSEG, int MODE>
 void launch_one(const KParams& kp, const double* theta, int64_t ld, const int32_t* cell_id, const uint8_t* active,
                 int64_t B, double* out0, double* out1, int64_t ld_out, hipStream_t stream) {
-  constexpr int WPB = Shape<RPL, NSEG>::kWaves;
-  const dim3 block(64 * WPB);
-  const dim3 grid((unsigned)((B + WPB - 1) / WPB));
+  const dim3 block(64 * kWavesPerBlock);
+  const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock));
   hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE>), grid, block, 0, stream, kp, theta, ld, cell_id, active, B,
                      out0, out1, ld_out);
 }
