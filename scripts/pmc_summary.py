@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (scripts/gpu_pmc.sh) for the likelihood kernel.
+
+HBM traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes, following
+MI355X_MICROARCH.md's HBM/rocprofv3 section: FETCH_SIZE (KB) reads 1/2 of the bytes of a wide
+coalesced read on gfx950; WRITE_SIZE is exact for streaming stores. The x2 read correction is
+calibrated for 16-B-per-lane reads; this kernel's theta reads are 8-16 B per lane (noted).
+Usage: python scripts/pmc_summary.py gpurun_out/<tag> <workload> > profiles/pmc_traffic.json
+"""
+import collections
+import csv
+import json
+import sys
+
+
+def main(prefix, workload):
+    agg = collections.defaultdict(list)
+    for p in range(1, 5):
+        try:
+            rows = list(csv.DictReader(open(f"{prefix}_p{p}/pmc_counter_collection.csv")))
+        except OSError:
+            continue
+        for r in rows:
+            if "tci_cohort_kernel" in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    mean = {k: sum(v) / len(v) for k, v in agg.items()}
+    fetch, write = mean.get("FETCH_SIZE"), mean.get("WRITE_SIZE")
+    out = {
+        "workload": workload,
+        "source": prefix,
+        "hbm_bytes_per_launch": None if fetch is None or write is None else (2 * fetch + write) * 1024,
+        "fetch_size_kb_raw": fetch,
+        "write_size_kb": write,
+        "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE reads 1/2 of wide streaming reads; "
+                      "calibrated for 16-B/lane reads, theta rows here are read 8-16 B/lane)",
+        "counters_mean_per_launch": mean,
+    }
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
