@@ -134,11 +134,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    # Rehearsal switch (never used by the driver): several ranks on ONE GPU over gloo.
+    rehearsal = os.environ.get("TCI_BENCH_REHEARSAL") == "1"
+    device_index = 0 if rehearsal else local
+    backend = "gloo" if rehearsal else "nccl"  # "nccl" is RCCL on ROCm
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(device_index)
+        if backend == "nccl":
+            dist.init_process_group(backend, rank=rank, world_size=world, device_id=torch.device("cuda", device_index))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+    dev = torch.device("cuda", device_index)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
     from transcriptioncycleinference_amd import Likelihood, testdata
 
@@ -146,7 +154,7 @@ def main():
     theta, cid, active = proposal_batch(cells, args.proposals, seed=20201028 + rank)
     B, ld = theta.shape
     n_active = int(active.sum())
-    lk = Likelihood(cells, CONSTRUCT, device=local)
+    lk = Likelihood(cells, CONSTRUCT, device=device_index)
     th_d = torch.from_numpy(theta).to(dev)
     cid_d = torch.from_numpy(cid).to(dev)
     act_d = torch.from_numpy(active).to(dev)
@@ -179,17 +187,17 @@ def main():
     ss = out_d.cpu().numpy()
     finite_ok = bool(np.all(np.isfinite(ss[active.astype(bool)])))
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        cnt = torch.tensor([n_active], dtype=torch.int64, device=dev)
+        cnt = torch.tensor([n_active], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
         total_active = int(cnt.item())
         # the one results collective: per-cell SS of the last proposal of every cell (RCCL)
         from transcriptioncycleinference_amd.parallel import gather_rows
 
         per_cell = ss.reshape(cells.n_cells, -1)[:, -1].copy()
-        gathered = gather_rows(per_cell, device=f"cuda:{local}")
+        gathered = gather_rows(per_cell, device=str(coll_dev))
         assert len(gathered) == cells.n_cells * world
     else:
         total_active = n_active
@@ -234,6 +242,17 @@ def main():
         },
         "results_finite": finite_ok,
     }
+    if rank == 0 and world == 1:
+        # PCIe-inclusive rate of the host-pointer entry point (theta H2D + SS D2H per call):
+        # reported beside, never as, `value`.
+        lk.ss_batch(theta, cid, active)
+        h0 = time.perf_counter()
+        for _ in range(3):
+            lk.ss_batch(theta, cid, active)
+        h_el = (time.perf_counter() - h0) / 3
+        res["host_api_pcie_inclusive"] = {"value": n_active / h_el, "unit": "SS evals/s",
+                                          "ms_per_call": h_el * 1e3, "bytes_h2d": int(theta.nbytes + cid.nbytes
+                                                                                    + active.nbytes)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cells, theta, cid, active, args.cpu_seconds)
     if rank == 0:

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""A/B timing of kernel build variants, interleaved in ONE process (cdna_hip_programming.md
+§5.4 rule 24). Build here:  python scripts/ab_variants.py --build
+Run on the GPU box:         python scripts/ab_variants.py --run [--rounds 9 --launches 20]
+Every variant is also checked against the shipped build (rel <= 1e-12)."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "build", "ab")
+
+VARIANTS = {
+    "ship": [],
+    "w6": ["TCI_WAVES_PER_EU=6"],
+    "w6_noxcd": ["TCI_WAVES_PER_EU=6", "TCI_XCD_REMAP=0"],
+    "w7": ["TCI_WAVES_PER_EU=7"],
+    "w5": ["TCI_WAVES_PER_EU=5"],
+    "w8_latepts": ["TCI_WAVES_PER_EU=8", "TCI_EARLY_POINTS=0"],
+    "w6_latepts_noxcd": ["TCI_WAVES_PER_EU=6", "TCI_EARLY_POINTS=0", "TCI_XCD_REMAP=0"],
+    "noxcd": ["TCI_XCD_REMAP=0"],
+    "loopramp": ["TCI_RAMP_PREFIX=0"],
+    "latepts": ["TCI_EARLY_POINTS=0"],
+    "w8": ["TCI_WAVES_PER_EU=8"],
+}
+
+
+def build(names):
+    from transcriptioncycleinference_amd.build import build_library
+
+    os.makedirs(OUT, exist_ok=True)
+    for n in names:
+        build_library(out=os.path.join(OUT, f"libtci_{n}.so"), defines=VARIANTS[n], verbose=True)
+
+
+def run(names, rounds, launches, proposals):
+    import torch
+
+    import bench
+    from transcriptioncycleinference_amd import Likelihood, testdata
+
+    cells = testdata()
+    theta, cid, active = bench.proposal_batch(cells, proposals, seed=20201028)
+    dev = torch.device("cuda", 0)
+    th_d = torch.from_numpy(theta).to(dev)
+    cid_d = torch.from_numpy(cid).to(dev)
+    act_d = torch.from_numpy(active).to(dev)
+    lks = {n: Likelihood(cells, bench.CONSTRUCT, 0, lib_path=os.path.join(OUT, f"libtci_{n}.so")) for n in names}
+    outs = {n: torch.empty(len(cid), dtype=torch.float64, device=dev) for n in names}
+    st = torch.cuda.current_stream(dev)
+    for n in names:  # warm + correctness
+        lks[n].ss_batch_device(th_d, cid_d, outs[n], act_d, stream=st)
+    torch.cuda.synchronize()
+    ref = outs[names[0]].cpu().numpy()
+    act = active.astype(bool)
+    times = {n: [] for n in names}
+    for _ in range(rounds):
+        for n in names:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(launches):
+                lks[n].ss_batch_device(th_d, cid_d, outs[n], act_d, stream=st)
+            e1.record(st)
+            torch.cuda.synchronize()
+            times[n].append(e0.elapsed_time(e1) / launches * 1e3)
+    res = {}
+    for n in names:
+        got = outs[n].cpu().numpy()
+        rel = float(np.max(np.abs(got[act] - ref[act]) / np.abs(ref[act])))
+        t = np.array(times[n])
+        res[n] = {"median_us": float(np.median(t)), "min_us": float(t.min()), "rel_vs_first": rel,
+                  "evals_per_s": float(act.sum() / (np.median(t) * 1e-6)), "defines": VARIANTS[n]}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--run", action="store_true")
+    ap.add_argument("--variants", default="ship,w6,w6_noxcd,w7,w5,w8_latepts,w6_latepts_noxcd")
+    ap.add_argument("--rounds", type=int, default=9)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--proposals", type=int, default=256)
+    a = ap.parse_args()
+    names = a.variants.split(",")
+    if a.build:
+        build(names)
+    if a.run:
+        run(names, a.rounds, a.launches, a.proposals)

@@ -34,16 +34,18 @@ def needs_rebuild() -> bool:
     return any(os.path.getmtime(s) > t for s in SOURCES + HEADERS + [__file__])
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_rebuild():
+def build_library(force: bool = False, verbose: bool = False, out: str = LIB, defines=None) -> str:
+    """Compile libtci.so (or an A/B variant with extra -D defines into `out`)."""
+    if out == LIB and not defines and not force and not needs_rebuild():
         return LIB
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wall", "-Wno-bitwise-instead-of-logical", "-I" + os.path.join(REPO_ROOT, "include"), "-I" + CSRC, *SOURCES, "-o", LIB + ".tmp"]
+           "-Wall", "-Wno-bitwise-instead-of-logical", "-I" + os.path.join(REPO_ROOT, "include"), "-I" + CSRC,
+           *[f"-D{d}" for d in (defines or [])], *SOURCES, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

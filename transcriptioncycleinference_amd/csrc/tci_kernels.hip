@@ -48,6 +48,25 @@
 
 #include "tci_internal.h"
 
+// Build-time variants for A/B timing (scripts/ab_variants.py); the shipped defaults are below.
+#ifndef TCI_XCD_REMAP
+#define TCI_XCD_REMAP 0      // XCD-aware block -> row-range order (A/B: ~1% slower here; the
+#endif                       // 3.7 MB cell table fits every XCD's L2 anyway)
+#ifndef TCI_RAMP_PREFIX
+#define TCI_RAMP_PREFIX 1    // O(1) ramp via the J prefix table (else a loop over ramp distances)
+#endif
+#ifndef TCI_EARLY_POINTS
+#define TCI_EARLY_POINTS 1   // issue the acquisition-point loads with the first round trip
+#endif
+#ifndef TCI_WAVES_PER_EU
+#define TCI_WAVES_PER_EU 6   // register budget for 6 waves/SIMD (A/B: 50 us vs 58 us at the
+#endif                       // compiler's default 5 waves; 7-8 waves no faster)
+#if TCI_WAVES_PER_EU > 0
+#define TCI_OCCUPANCY __attribute__((amdgpu_waves_per_eu(TCI_WAVES_PER_EU)))
+#else
+#define TCI_OCCUPANCY
+#endif
+
 namespace tci {
 
 namespace {
@@ -111,20 +130,34 @@ struct Regions {
   int r_lo, r_hi, f_lo, f_hi;
 };
 
-// Row sum of one segment of one dye on the fast path (see the header): K table in LDS at
-// Ktab[i] = K_i (K_i = 0 for i < 0).
-__device__ __forceinline__ double row_sum(const double* Ktab, int r, const Regions& rg, const SegParams& s,
+// Exact prefix tables of the fast path, interleaved per cohort index i (LDS, 16 B per entry):
+//   K_i = sum_{i' <= i} c_i'        (= floor(counter_i): polymerases loaded through step i)
+//   J_i = sum_{i' <= i} i' * c_i'
+// Both are integers < 2^53, exact in any summation order. Entry 0 holds i = -1 (zeros).
+__device__ __forceinline__ double2 kj_at(const double2* KJ, int i) { return KJ[(i < -1 ? -1 : i) + 1]; }
+
+// Row sum of one segment of one dye on the fast path (see the header), O(1) per row:
+//   full  (e < P_m < L, m in [f_lo, f_hi]):  phi * (K[r - f_lo] - K[r - f_hi - 1])
+//   ramp  (a < P_m < e, m in [r_lo, r_hi]):  sum_m c_{r-m} * (m*vd0 - a) * k
+//        = k * (vd0 * sum_m m*c_{r-m}  -  a * sum_m c_{r-m}),   sum_m m*c_{r-m} = r*C - (J_hi - J_lo)
+__device__ __forceinline__ double row_sum(const double2* KJ, int r, const Regions& rg, const SegParams& s,
                                           double vd0) {
   double acc = 0.0;
-  if (rg.f_lo <= rg.f_hi) acc = s.phi * (Ktab[r - rg.f_lo] - Ktab[r - rg.f_hi - 1]);
+  if (rg.f_lo <= rg.f_hi) acc = s.phi * (kj_at(KJ, r - rg.f_lo).x - kj_at(KJ, r - rg.f_hi - 1).x);
   if (rg.r_lo <= rg.r_hi) {
-    double kA = Ktab[r - rg.r_lo];
+#if TCI_RAMP_PREFIX
+    const double2 hi = kj_at(KJ, r - rg.r_lo), lo = kj_at(KJ, r - rg.r_hi - 1);
+    const double C = hi.x - lo.x;
+    const double Mc = (double)r * C - (hi.y - lo.y);  // sum of m * c_{r-m}, exact
+    acc += s.k * (vd0 * Mc - s.a * C);
+#else
+    double kA = kj_at(KJ, r - rg.r_lo).x;
     for (int m = rg.r_lo; m <= rg.r_hi; ++m) {
-      const double kB = Ktab[r - m - 1];
-      const double F = ((double)m * vd0 - s.a) * s.k;
-      acc = fma(kA - kB, F, acc);
+      const double kB = kj_at(KJ, r - m - 1).x;
+      acc = fma(kA - kB, ((double)m * vd0 - s.a) * s.k, acc);
       kA = kB;
     }
+#endif
   }
   return acc;
 }
@@ -139,21 +172,29 @@ __device__ __forceinline__ void write_nan(int lane, int N, int64_t b, double* ou
 }
 
 template <int RPL, int NSEG, int MODE>
-__global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
+__global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
                                                          int64_t ld_out) {
   constexpr int SLOTS = 64 * RPL;      // rows 1..SLOTS (row 0 never holds a polymerase)
-  constexpr int KOFF = SLOTS + 1;      // K table: Ktab[KOFF + i] = K_i, zeros below
   constexpr int SIMP = SLOTS + 2;      // offset of the PP7 row array
   constexpr int NPT = RPL + 1;         // acquisition points per lane (N <= 64*RPL + 1)
-  constexpr int WAVE_DOUBLES = 2 * SLOTS + 4;
-  __shared__ double s_lds[kWavesPerBlock][WAVE_DOUBLES];
+  constexpr int WAVE_DOUBLES = 2 * SLOTS + 4;  // {K,J} table (SLOTS+1 entries) / the two sim rows
+  __shared__ __attribute__((aligned(16))) double s_lds[kWavesPerBlock][WAVE_DOUBLES];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs; give each XCD a
+  // contiguous range of rows so rows of the same cell share one XCD's L2 (speed only).
+#if TCI_XCD_REMAP
+  const unsigned nb = gridDim.x, bid = blockIdx.x;
+  const unsigned xq = nb / 8, xr = nb % 8, xcd = bid % 8, xk = bid / 8;
+  const unsigned vb = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
+#else
+  const unsigned vb = blockIdx.x;
+#endif
+  const int64_t b = (int64_t)vb * kWavesPerBlock + wid;
   if (b >= B) return;
   double* lds = s_lds[wid];
   double* simM = lds;
@@ -185,14 +226,15 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
     st[q] = ST[g];                          // g < cell_stride
   }
   PointRec pt[NPT];
-  if (MODE != MODE_FWD_RAW) {
+  auto load_points = [&]() {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int j = lane + 64 * k;
       if (j <= SLOTS) pt[k] = PT[j];
       else pt[k] = PointRec{0.0, 0.0, 0.0, -1.0};
     }
-  }
+  };
+  if (TCI_EARLY_POINTS && MODE != MODE_FWD_RAW) load_points();
   const int N = cm.n;
   if (ld < 7 + N) {
     write_nan<MODE>(lane, N, b, out0, out1, ld_out);
@@ -319,22 +361,31 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
       }
     }
     if (fast) {
-      // ---- K table (exact cumulative loaded counts) and O(1 + ramp) row sums
-      double* Ktab = lds + KOFF;
+      // ---- {K, J} prefix tables (exact) and O(1) row sums
+      double jloc[RPL], js = 0.0;
+      {
+        const double kprev = wave_shr1(K[RPL - 1]);
 #pragma unroll
-      for (int q = 0; q < RPL; ++q) {
-        lds[RPL * lane + q] = 0.0;
-        Ktab[RPL * lane + q] = K[q];
+        for (int q = 0; q < RPL; ++q) {
+          const int g = RPL * lane + q;
+          const double cg = g < nsteps ? K[q] - (q == 0 ? kprev : K[q - 1]) : 0.0;
+          js = js + (double)g * cg;
+          jloc[q] = js;
+        }
       }
-      if (lane == 0) lds[SLOTS] = 0.0;
+      const double jexcl = wave_shr1(wave_incl_scan(js));
+      double2* KJ = reinterpret_cast<double2*>(lds);
+#pragma unroll
+      for (int q = 0; q < RPL; ++q) KJ[RPL * lane + q + 1] = make_double2(K[q], jexcl + jloc[q]);
+      if (lane == 0) KJ[0] = make_double2(0.0, 0.0);
       wave_sync();
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {
         const int r = RPL * lane + q + 1;
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) {
-          accM[k][q] = row_sum(Ktab, r, rgM[k], sm[k], vd0);
-          accP[k][q] = row_sum(Ktab, r, rgP[k], sp[k], vd0);
+          accM[k][q] = row_sum(KJ, r, rgM[k], sm[k], vd0);
+          accP[k][q] = row_sum(KJ, r, rgP[k], sp[k], vd0);
         }
       }
     } else {
@@ -377,7 +428,7 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
       }
     }
   }
-  wave_sync();  // every K-table read is done before the rows overwrite the LDS
+  wave_sync();  // every {K,J}-table read is done before the rows overwrite the LDS
 
   // ---- basal floor inside the segment loop (GetFluorFromPolPos.m:54-57,66-69), x A (SumofSquares...m:51)
 #pragma unroll
@@ -418,9 +469,11 @@ __global__ __launch_bounds__(256) void tci_cohort_kernel(const KParams kp, const
 
   // ---- interp1 back to the acquisition times (SumofSquares...m:55-56) and nansum of the
   //      squared residuals over [MS2, PP7] (:57-64).
+  if (!TCI_EARLY_POINTS) load_points();
   double ss = 0.0;
 #pragma unroll
   for (int kk = 0; kk < NPT; ++kk) {
+    if (kk == RPL && N <= 64 * RPL) break;  // uniform: only N = 64*RPL + 1 has a tail point
     const int j = lane + 64 * kk;
     if (j < N) {
       const int k = (int)pt[kk].k;

@@ -19,8 +19,9 @@ from .data import Cells
 class Likelihood:
     """SS evaluator bound to one device and one dataset (the C ``tci_ctx``)."""
 
-    def __init__(self, cells: Cells, construct="P2P-MS2v5-LacZ-PP7v4", device: int = 0):
-        self._lib = _lib.load()
+    def __init__(self, cells: Cells, construct="P2P-MS2v5-LacZ-PP7v4", device: int = 0,
+                 lib_path: Optional[str] = None):
+        self._lib = _lib.load(lib_path)  # lib_path: an A/B build variant (default: libtci.so)
         self.cells = cells
         self.construct: Construct = as_construct(construct)
         self.device = int(device)
