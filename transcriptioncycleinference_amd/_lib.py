@@ -55,6 +55,19 @@ class tci_info(C.Structure):
                 ("max_points", C.c_int64), ("device_bytes", C.c_int64)]
 
 
+class tci_dram_options(C.Structure):
+    _fields_ = [("n_steps", C.c_int64), ("burnintime", C.c_int64), ("adaptint", C.c_int64), ("ntry", C.c_int32),
+                ("updatesigma", C.c_int32), ("drscale", C.c_double), ("adascale", C.c_double),
+                ("qcovadj", C.c_double), ("burnin_scale", C.c_double), ("stats_from", C.c_int64),
+                ("thin", C.c_int64), ("seed", C.c_uint64)]
+
+
+class tci_dram_outputs(C.Structure):
+    _fields_ = [("mean", _dp), ("std", _dp), ("final_theta", _dp), ("sigma_mean", _dp), ("sigma_std", _dp),
+                ("accept_rate", _dp), ("n_evals", _i64p), ("chain", _dp), ("s2chain", _dp),
+                ("elapsed_ms", C.c_double)]
+
+
 # (name, restype, argtypes) for every symbol declared in include/tci.h
 SIGNATURES = [
     ("tci_construct_by_name", C.c_int, [C.c_char_p, C.POINTER(tci_construct)]),
@@ -70,6 +83,9 @@ SIGNATURES = [
     ("tci_forward", C.c_int, [C.c_void_p, _dp, C.c_int64, _i32p, C.c_int64, C.c_int, _dp, _dp, C.c_int64]),
     ("tci_cell_points", C.c_int, [C.c_void_p, C.c_int32, _i64p]),
     ("tci_cell_grid", C.c_int, [C.c_void_p, C.c_int32, _dp, C.c_int64, _i64p]),
+    ("tci_dram_defaults", C.c_int, [C.POINTER(tci_dram_options)]),
+    ("tci_dram_run", C.c_int, [C.c_void_p, C.POINTER(tci_dram_options), C.c_int64, _i32p, _dp, _dp, _dp, _dp, _dp,
+                               _dp, _dp, C.c_int64, C.POINTER(tci_dram_outputs)]),
     ("tci_version", C.c_char_p, []),
 ]
 

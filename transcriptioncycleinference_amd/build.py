@@ -14,8 +14,9 @@ import sys
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_ROOT = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
-SOURCES = [os.path.join(CSRC, "tci_kernels.hip"), os.path.join(CSRC, "tci_api.cpp")]
-HEADERS = [os.path.join(REPO_ROOT, "include", "tci.h"), os.path.join(CSRC, "tci_internal.h")]
+SOURCES = [os.path.join(CSRC, "tci_kernels.hip"), os.path.join(CSRC, "tci_dram.hip"), os.path.join(CSRC, "tci_api.cpp")]
+HEADERS = [os.path.join(REPO_ROOT, "include", "tci.h"), os.path.join(CSRC, "tci_internal.h"),
+           os.path.join(CSRC, "tci_dram_internal.h")]
 LIB = os.path.join(PKG_DIR, "libtci.so")
 ARCH = os.environ.get("TCI_OFFLOAD_ARCH", "gfx950")
 

@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "tci_dram_internal.h"
 #include "tci_internal.h"
 
 using tci::CellMeta;
@@ -440,6 +441,258 @@ int tci_cell_grid(const tci_ctx* ctx, int32_t cell, double* t_interp_out, int64_
   if (!t_interp_out) return TCI_OK;
   if (cap < m.n) return TCI_ERANGE;
   std::memcpy(t_interp_out, ctx->grid.data() + (size_t)cell * (size_t)ctx->stride, (size_t)m.n * sizeof(double));
+  return TCI_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Device allocations of one DRAM run, freed together.
+struct DevAllocs {
+  std::vector<void*> ptrs;
+  ~DevAllocs() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  template <typename T>
+  T* alloc(size_t n, hipError_t* err) {
+    void* p = nullptr;
+    *err = hipMalloc(&p, std::max(n, (size_t)1) * sizeof(T));
+    if (*err == hipSuccess) ptrs.push_back(p);
+    return (T*)p;
+  }
+};
+
+// One DRAM step: propose -> ssfun -> accept/propose stage 2 -> ssfun -> accept, sigma2, record
+// -> adapt (no-op unless step % adaptint == 0) -> step + 1.
+int enqueue_step(tci_ctx* ctx, const tci::DramState& st, const tci::DramParams& p, hipStream_t s) {
+  int rc;
+  if ((rc = tci::dram_launch_propose1(st, p, s)) != TCI_OK) return rc;
+  if ((rc = tci::launch(ctx->kp, ctx->rpl, tci::MODE_SS, st.prop1, st.ld, st.cell, st.act1, st.n_chains, st.ss1,
+                        nullptr, 0, s)) != TCI_OK)
+    return rc;
+  if ((rc = tci::dram_launch_accept1(st, p, s)) != TCI_OK) return rc;
+  if (p.ntry >= 2 && (rc = tci::launch(ctx->kp, ctx->rpl, tci::MODE_SS, st.prop2, st.ld, st.cell, st.act2,
+                                       st.n_chains, st.ss2, nullptr, 0, s)) != TCI_OK)
+    return rc;
+  if ((rc = tci::dram_launch_accept2(st, p, s)) != TCI_OK) return rc;
+  if ((rc = tci::dram_launch_adapt(st, p, s)) != TCI_OK) return rc;
+  return tci::dram_launch_step_incr(st, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int tci_dram_defaults(tci_dram_options* o) {
+  if (!o) return TCI_EINVAL;
+  o->n_steps = 20000;     // TranscriptionCycleMCMC.m:40
+  o->burnintime = 10000;  // :39, :267
+  o->adaptint = 100;      // :268
+  o->ntry = 2;            // 'dram' (:269)
+  o->updatesigma = 1;     // :265
+  o->drscale = 5.0;
+  o->adascale = 0.0;
+  o->qcovadj = 1e-5;
+  o->burnin_scale = 10.0;
+  o->stats_from = 10000;  // chain(n_burn:end, :) (:276)
+  o->thin = 0;
+  o->seed = 20201028;
+  return TCI_OK;
+}
+
+int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, const int32_t* cell_id,
+                 const double* theta0, const double* lower, const double* upper, const double* prior_mu,
+                 const double* prior_sig, const double* qcov_diag, const double* sigma2_0, int64_t ld,
+                 tci_dram_outputs* out) {
+  if (!ctx) return TCI_EINVAL;
+  if (!opt || !out || n_chains <= 0 || !cell_id || !theta0 || !lower || !upper || !prior_mu || !prior_sig ||
+      !qcov_diag || !sigma2_0)
+    return fail(ctx, TCI_EINVAL, "tci_dram_run: null argument or no chains");
+  if (opt->n_steps < 1 || opt->ntry < 1 || opt->ntry > 2 || opt->adaptint < 0 || !(opt->drscale > 0))
+    return fail(ctx, TCI_EINVAL, "tci_dram_run: bad options (n_steps >= 1, ntry in {1,2}, adaptint >= 0)");
+  int rc = check_rows(ctx, ld, cell_id, n_chains);
+  if (rc != TCI_OK) return rc;
+  if (ld > TCI_MAX_POINTS + 7) return fail(ctx, TCI_ERANGE, "tci_dram_run: ld too large");
+  const size_t n = (size_t)n_chains, L = (size_t)ld, L2 = L * L;
+  std::vector<int32_t> npar(n), nobs(n);
+  for (size_t c = 0; c < n; ++c) {
+    const int32_t N = ctx->meta[(size_t)cell_id[c]].n;
+    npar[c] = 7 + N;
+    nobs[c] = 2 * N;  // model.N = length(data.ydata) (:260), NaNs included
+    for (int32_t j = 0; j < npar[c]; ++j) {
+      const double x = theta0[c * L + j];
+      if (!(x >= lower[c * L + j] && x <= upper[c * L + j]))
+        return fail(ctx, TCI_EINVAL, "tci_dram_run: chain " + std::to_string(c) + " starts outside its bounds");
+      if (!(qcov_diag[c * L + j] > 0)) return fail(ctx, TCI_EINVAL, "tci_dram_run: qcov_diag must be > 0");
+    }
+  }
+  TCI_HIP(ctx, hipSetDevice(ctx->device));
+  DevAllocs A;
+  hipError_t e = hipSuccess;
+  tci::DramState st{};
+  tci::DramParams p{};
+  const int64_t win = std::max<int64_t>(opt->adaptint, 1);
+  const int64_t n_keep = opt->thin > 0 ? (opt->n_steps + opt->thin - 1) / opt->thin : 0;
+  st.n_chains = n_chains;
+  st.ld = ld;
+#define TCI_ALLOC(field, T, count)                                  \
+  do {                                                              \
+    st.field = A.alloc<T>((count), &e);                             \
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dram " #field ")"); \
+  } while (0)
+  int32_t *d_cell, *d_npar, *d_nobs;
+  double *d_lower, *d_upper, *d_pmu, *d_psig, *d_qdiag, *d_s20;
+  d_cell = A.alloc<int32_t>(n, &e);
+  d_npar = A.alloc<int32_t>(n, &e);
+  d_nobs = A.alloc<int32_t>(n, &e);
+  d_lower = A.alloc<double>(n * L, &e);
+  d_upper = A.alloc<double>(n * L, &e);
+  d_pmu = A.alloc<double>(n * L, &e);
+  d_psig = A.alloc<double>(n * L, &e);
+  d_qdiag = A.alloc<double>(n * L, &e);
+  d_s20 = A.alloc<double>(n, &e);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dram inputs)");
+  st.cell = d_cell;
+  st.npar = d_npar;
+  st.nobs = d_nobs;
+  st.lower = d_lower;
+  st.upper = d_upper;
+  st.pmu = d_pmu;
+  st.psig = d_psig;
+  TCI_ALLOC(theta, double, n * L);
+  TCI_ALLOC(ss, double, n);
+  TCI_ALLOC(prior, double, n);
+  TCI_ALLOC(sigma2, double, n);
+  TCI_ALLOC(R, double, n * L2);
+  TCI_ALLOC(iR, double, n * L2);
+  TCI_ALLOC(cov, double, n * L2);
+  TCI_ALLOC(work, double, n * L2);
+  TCI_ALLOC(cmean, double, n * L);
+  TCI_ALLOC(wsum, double, n);
+  TCI_ALLOC(window, double, n * (size_t)win * L);
+  TCI_ALLOC(prop1, double, n * L);
+  TCI_ALLOC(prop2, double, n * L);
+  TCI_ALLOC(act1, uint8_t, n);
+  TCI_ALLOC(act2, uint8_t, n);
+  TCI_ALLOC(acc1, uint8_t, n);
+  TCI_ALLOC(ss1, double, n);
+  TCI_ALLOC(ss2, double, n);
+  TCI_ALLOC(prior1, double, n);
+  TCI_ALLOC(a12, double, n);
+  TCI_ALLOC(naccept, int32_t, n);
+  TCI_ALLOC(nrej_win, int32_t, n);
+  TCI_ALLOC(nevals, int64_t, n);
+  TCI_ALLOC(smean, double, n * L);
+  TCI_ALLOC(sm2, double, n * L);
+  TCI_ALLOC(s2sum, double, n);
+  TCI_ALLOC(sq_mean, double, n);
+  TCI_ALLOC(sq_m2, double, n);
+  TCI_ALLOC(step, int64_t, 1);
+  if (n_keep > 0 && (out->chain || out->s2chain)) {
+    TCI_ALLOC(chain_out, double, (size_t)n_keep * n * L);
+    TCI_ALLOC(s2_out, double, (size_t)n_keep * n);
+  }
+#undef TCI_ALLOC
+  hipStream_t s = ctx->stream;
+  TCI_HIP(ctx, hipMemcpyAsync(d_cell, cell_id, n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  TCI_HIP(ctx, hipMemcpyAsync(d_npar, npar.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  TCI_HIP(ctx, hipMemcpyAsync(d_nobs, nobs.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  TCI_HIP(ctx, hipMemcpyAsync(d_lower, lower, n * L * sizeof(double), hipMemcpyHostToDevice, s));
+  TCI_HIP(ctx, hipMemcpyAsync(d_upper, upper, n * L * sizeof(double), hipMemcpyHostToDevice, s));
+  TCI_HIP(ctx, hipMemcpyAsync(d_pmu, prior_mu, n * L * sizeof(double), hipMemcpyHostToDevice, s));
+  TCI_HIP(ctx, hipMemcpyAsync(d_psig, prior_sig, n * L * sizeof(double), hipMemcpyHostToDevice, s));
+  TCI_HIP(ctx, hipMemcpyAsync(d_qdiag, qcov_diag, n * L * sizeof(double), hipMemcpyHostToDevice, s));
+  TCI_HIP(ctx, hipMemcpyAsync(d_s20, sigma2_0, n * sizeof(double), hipMemcpyHostToDevice, s));
+  TCI_HIP(ctx, hipMemcpyAsync(st.theta, theta0, n * L * sizeof(double), hipMemcpyHostToDevice, s));
+  TCI_HIP(ctx, hipMemsetAsync(st.wsum, 0, n * sizeof(double), s));
+  TCI_HIP(ctx, hipMemsetAsync(st.act2, 0, n, s));
+  p.seed = opt->seed;
+  p.ntry = opt->ntry;
+  p.updatesigma = opt->updatesigma;
+  p.drscale = opt->drscale;
+  p.adascale = opt->adascale;
+  p.qcovadj = opt->qcovadj;
+  p.burnin_scale = opt->burnin_scale;
+  p.adaptint = opt->adaptint;
+  p.burnintime = opt->burnintime;
+  p.stats_from = std::max<int64_t>(opt->stats_from, 1);
+  p.thin = opt->thin;
+  p.n_keep = n_keep;
+  // initial state: R = chol(J0), prior, sigma2, the initial ssfun call, chain row 1
+  if ((rc = tci::dram_launch_init(st, d_qdiag, d_s20, s)) != TCI_OK) return fail(ctx, rc, "dram init launch");
+  if ((rc = tci::launch(ctx->kp, ctx->rpl, tci::MODE_SS, st.theta, ld, d_cell, nullptr, n_chains, st.ss, nullptr, 0,
+                        s)) != TCI_OK)
+    return fail(ctx, rc, "initial ssfun launch");
+  if ((rc = tci::dram_launch_init_stats(st, p, s)) != TCI_OK) return fail(ctx, rc, "dram stats launch");
+  const int64_t two = 2;
+  TCI_HIP(ctx, hipMemcpyAsync(st.step, &two, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  hipEvent_t ev0, ev1;
+  TCI_HIP(ctx, hipEventCreate(&ev0));
+  TCI_HIP(ctx, hipEventCreate(&ev1));
+  TCI_HIP(ctx, hipEventRecord(ev0, s));
+  // the step loop: blocks of G steps captured once as a hipGraph and replayed
+  const int64_t total = opt->n_steps - 1, G = 50;
+  const int64_t blocks = total / G, rest = total % G;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  if (blocks > 0) {
+    TCI_HIP(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    int crc = TCI_OK;
+    for (int64_t k = 0; k < G && crc == TCI_OK; ++k) crc = enqueue_step(ctx, st, p, s);
+    hipError_t ce = hipStreamEndCapture(s, &graph);
+    if (crc != TCI_OK || ce != hipSuccess) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return fail(ctx, TCI_EHIP, "DRAM step graph capture failed");
+    }
+    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+      (void)hipGraphDestroy(graph);
+      return hip_fail(ctx, e, "hipGraphInstantiate");
+    }
+    for (int64_t b = 0; b < blocks && e == hipSuccess; ++b) e = hipGraphLaunch(exec, s);
+  }
+  for (int64_t k = 0; k < rest && rc == TCI_OK && e == hipSuccess; ++k) rc = enqueue_step(ctx, st, p, s);
+  const hipError_t ge = e;
+  TCI_HIP(ctx, hipEventRecord(ev1, s));
+  TCI_HIP(ctx, hipStreamSynchronize(s));
+  if (exec) (void)hipGraphExecDestroy(exec);
+  if (graph) (void)hipGraphDestroy(graph);
+  if (ge != hipSuccess) return hip_fail(ctx, ge, "DRAM step replay");
+  if (rc != TCI_OK) return fail(ctx, rc, "DRAM step launch");
+  float ms = 0.f;
+  TCI_HIP(ctx, hipEventElapsedTime(&ms, ev0, ev1));
+  (void)hipEventDestroy(ev0);
+  (void)hipEventDestroy(ev1);
+  out->elapsed_ms = ms;
+  // ---- outputs
+  std::vector<double> smean(n * L), sm2(n * L), s2sum(n), sqm(n), sqm2(n);
+  std::vector<int32_t> nacc(n);
+  std::vector<int64_t> nev(n);
+  TCI_HIP(ctx, hipMemcpy(smean.data(), st.smean, n * L * sizeof(double), hipMemcpyDeviceToHost));
+  TCI_HIP(ctx, hipMemcpy(sm2.data(), st.sm2, n * L * sizeof(double), hipMemcpyDeviceToHost));
+  TCI_HIP(ctx, hipMemcpy(s2sum.data(), st.s2sum, n * sizeof(double), hipMemcpyDeviceToHost));
+  TCI_HIP(ctx, hipMemcpy(sqm.data(), st.sq_mean, n * sizeof(double), hipMemcpyDeviceToHost));
+  TCI_HIP(ctx, hipMemcpy(sqm2.data(), st.sq_m2, n * sizeof(double), hipMemcpyDeviceToHost));
+  TCI_HIP(ctx, hipMemcpy(nacc.data(), st.naccept, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  TCI_HIP(ctx, hipMemcpy(nev.data(), st.nevals, n * sizeof(int64_t), hipMemcpyDeviceToHost));
+  const double nrow_stats = (double)std::max<int64_t>(opt->n_steps - p.stats_from + 1, 0);
+  for (size_t c = 0; c < n; ++c) {
+    for (size_t j = 0; j < L; ++j) {
+      if (out->mean) out->mean[c * L + j] = (int64_t)j < npar[c] && nrow_stats > 0 ? smean[c * L + j] : NAN;
+      if (out->std)
+        out->std[c * L + j] = (int64_t)j < npar[c] && nrow_stats > 0 ? std::sqrt(sm2[c * L + j] / nrow_stats) : NAN;
+    }
+    if (out->sigma_mean) out->sigma_mean[c] = std::sqrt(s2sum[c] / (double)opt->n_steps);
+    if (out->sigma_std) out->sigma_std[c] = std::sqrt(sqm2[c] / (double)opt->n_steps);
+    if (out->accept_rate) out->accept_rate[c] = opt->n_steps > 1 ? nacc[c] / (double)(opt->n_steps - 1) : 0.0;
+    if (out->n_evals) out->n_evals[c] = nev[c];
+  }
+  if (out->final_theta) TCI_HIP(ctx, hipMemcpy(out->final_theta, st.theta, n * L * sizeof(double), hipMemcpyDeviceToHost));
+  if (st.chain_out && out->chain)
+    TCI_HIP(ctx, hipMemcpy(out->chain, st.chain_out, (size_t)n_keep * n * L * sizeof(double), hipMemcpyDeviceToHost));
+  if (st.s2_out && out->s2chain)
+    TCI_HIP(ctx, hipMemcpy(out->s2chain, st.s2_out, (size_t)n_keep * n * sizeof(double), hipMemcpyDeviceToHost));
   return TCI_OK;
 }
 

@@ -1,0 +1,78 @@
+// tci_dram_internal.h -- device state of the GPU-resident batched DRAM sampler.
+#pragma once
+
+#include <stdint.h>
+
+#include "tci.h"
+
+namespace tci {
+
+// All arrays are indexed by chain c; vectors have stride ld (= max parameter count P_max),
+// matrices stride ld*ld (row-major, P_c x P_c used).
+struct DramState {
+  int64_t n_chains;
+  int64_t ld;
+  const int32_t* cell;     // chain -> cell of the context
+  const int32_t* npar;     // P_c = 7 + N_c
+  const int32_t* nobs;     // N = length(ydata) = 2 N_c (TranscriptionCycleMCMC.m:260)
+  const double* lower;     // bounds (TranscriptionCycleMCMC.m:242-255)
+  const double* upper;
+  const double* pmu;       // Gaussian prior mean / sd (sd = +Inf: no prior), :254
+  const double* psig;
+  double* theta;           // current state
+  double* ss;              // SS of the current state
+  double* prior;           // prior SS of the current state
+  double* sigma2;          // error variance (model.sigma2, :259)
+  double* R;               // proposal Cholesky factor (upper): proposal = theta + z * R
+  double* iR;              // R^-1 (upper), for the delayed-rejection proposal ratio
+  double* cov;             // running chain covariance / mean / weight (mcmcstat covupd)
+  double* cmean;
+  double* wsum;
+  double* window;          // the last adaptint chain rows (for covupd)
+  double* prop1;           // stage-1 / stage-2 proposals (n_chains x ld)
+  double* prop2;
+  uint8_t* act1;           // in-bounds flags (ssfun is called only for these)
+  uint8_t* act2;
+  uint8_t* acc1;           // stage 1 accepted this step
+  double* ss1;             // SS of the proposals (+Inf when out of bounds)
+  double* ss2;
+  double* prior1;
+  double* a12;             // stage-1 acceptance probability
+  int32_t* naccept;        // accepted moves
+  int32_t* nrej_win;       // rejections in the current adaptation window (burn-in scaling)
+  int64_t* nevals;         // ssfun evaluations (in-bounds proposals)
+  double* smean;           // posterior mean / M2 (Welford) over rows >= stats_from
+  double* sm2;
+  double* s2sum;           // sum of s2 and Welford of sqrt(s2) over all rows (:302-303)
+  double* sq_mean;
+  double* sq_m2;
+  double* chain_out;       // optional thinned chain rows (n_keep x n_chains x ld) or null
+  double* s2_out;          // optional thinned s2 rows
+  double* work;            // Cholesky workspace (n_chains x ld x ld)
+  int64_t* step;           // current chain row (1-based), advanced on device after each step
+};
+
+struct DramParams {
+  uint64_t seed;
+  int32_t ntry;
+  int32_t updatesigma;
+  double drscale;
+  double adascale;  // <= 0: 2.4 / sqrt(P_c) per chain
+  double qcovadj;
+  double burnin_scale;
+  int64_t adaptint;
+  int64_t burnintime;
+  int64_t stats_from;
+  int64_t thin;
+  int64_t n_keep;
+};
+
+int dram_launch_init(const DramState& st, const double* qcov_diag, const double* sigma2_0, void* stream);
+int dram_launch_propose1(const DramState& st, const DramParams& p, void* stream);
+int dram_launch_accept1(const DramState& st, const DramParams& p, void* stream);
+int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream);
+int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream);  // no-op unless step % adaptint == 0
+int dram_launch_step_incr(const DramState& st, void* stream);
+int dram_launch_init_stats(const DramState& st, const DramParams& p, void* stream);
+
+}  // namespace tci
