@@ -122,6 +122,32 @@ __device__ double prior_ss(const double* th, const double* mu, const double* sig
   return wsum64(s);
 }
 
+// Column j of the row-vector product (v * M)_j = sum_{i<=j} v_i M[i][j] for an upper-triangular
+// row-major M (stride ld), for the 64 columns j0..j0+63 (one per lane). v in LDS. Eight
+// independent loads are issued per round so the L2/MALL latency overlaps (the wave is otherwise
+// latency-bound on one dependent load per term).
+__device__ __forceinline__ double tri_col(const double* v, const double* M, int64_t ld, int j0, int j, int P) {
+  const int imax = (j0 + 63 < P - 1 ? j0 + 63 : P - 1);  // uniform
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int i = 0;
+  for (; i + 7 <= imax; i += 8) {
+    double r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r[u] = (i + u <= j && j < P) ? M[(int64_t)(i + u) * ld + j] : 0.0;
+    a0 = fma(v[i + 0], r[0], a0);
+    a1 = fma(v[i + 1], r[1], a1);
+    a2 = fma(v[i + 2], r[2], a2);
+    a3 = fma(v[i + 3], r[3], a3);
+    a0 = fma(v[i + 4], r[4], a0);
+    a1 = fma(v[i + 5], r[5], a1);
+    a2 = fma(v[i + 6], r[6], a2);
+    a3 = fma(v[i + 7], r[7], a3);
+  }
+  for (; i <= imax; ++i)
+    if (i <= j && j < P) a0 = fma(v[i], M[(int64_t)i * ld + j], a0);
+  return (a0 + a1) + (a2 + a3);
+}
+
 // out[j] = base[j] + scale * sum_i z_i R[i][j] (R upper triangular, row-major ld); returns whether
 // every out[j] is inside [lo, hi]. z in LDS.
 __device__ bool propose(const double* base, const double* R, int64_t ld, const double* z, double scale, int P,
@@ -129,11 +155,7 @@ __device__ bool propose(const double* base, const double* R, int64_t ld, const d
   bool inb = true;
   for (int j0 = 0; j0 < P; j0 += 64) {
     const int j = j0 + lane;
-    double acc = 0.0;
-    const int imax = (j0 + 63 < P - 1 ? j0 + 63 : P - 1);
-    for (int i = 0; i <= imax; ++i) {
-      if (i <= j && j < P) acc = fma(z[i], R[(int64_t)i * ld + j], acc);
-    }
+    const double acc = tri_col(z, R, ld, j0, j, P);
     if (j < P) {
       const double v = base[j] + scale * acc;
       out[j] = v;
@@ -150,10 +172,7 @@ __device__ double mahal(const double* a, const double* b, const double* iR, int6
   double s = 0.0;
   for (int j0 = 0; j0 < P; j0 += 64) {
     const int j = j0 + lane;
-    double acc = 0.0;
-    const int imax = (j0 + 63 < P - 1 ? j0 + 63 : P - 1);
-    for (int i = 0; i <= imax; ++i)
-      if (i <= j && j < P) acc = fma(dl[i], iR[(int64_t)i * ld + j], acc);
+    const double acc = tri_col(dl, iR, ld, j0, j, P);
     if (j < P) s += acc * acc;
   }
   wave_sync();
