@@ -464,8 +464,8 @@ struct DevAllocs {
 };
 
 // One DRAM step: propose -> ssfun -> accept/propose stage 2 -> ssfun -> accept, sigma2, record
-// -> adapt (no-op unless step % adaptint == 0) -> step + 1.
-int enqueue_step(tci_ctx* ctx, const tci::DramState& st, const tci::DramParams& p, hipStream_t s) {
+// -> [adapt] -> step + 1.
+int enqueue_step(tci_ctx* ctx, const tci::DramState& st, const tci::DramParams& p, hipStream_t s, bool with_adapt) {
   int rc;
   if ((rc = tci::dram_launch_propose1(st, p, s)) != TCI_OK) return rc;
   if ((rc = tci::launch(ctx->kp, ctx->rpl, tci::MODE_SS, st.prop1, st.ld, st.cell, st.act1, st.n_chains, st.ss1,
@@ -476,7 +476,7 @@ int enqueue_step(tci_ctx* ctx, const tci::DramState& st, const tci::DramParams& 
                                        st.n_chains, st.ss2, nullptr, 0, s)) != TCI_OK)
     return rc;
   if ((rc = tci::dram_launch_accept2(st, p, s)) != TCI_OK) return rc;
-  if ((rc = tci::dram_launch_adapt(st, p, s)) != TCI_OK) return rc;
+  if (with_adapt && (rc = tci::dram_launch_adapt(st, p, s)) != TCI_OK) return rc;  // no-op unless step % adaptint == 0
   return tci::dram_launch_step_incr(st, s);
 }
 
@@ -631,15 +631,26 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_HIP(ctx, hipEventCreate(&ev0));
   TCI_HIP(ctx, hipEventCreate(&ev1));
   TCI_HIP(ctx, hipEventRecord(ev0, s));
-  // the step loop: blocks of G steps captured once as a hipGraph and replayed
-  const int64_t total = opt->n_steps - 1, G = 50;
-  const int64_t blocks = total / G, rest = total % G;
+  // The step loop. Steps 2 .. n_steps; adaptation after steps that are multiples of adaptint.
+  // Blocks of adaptint steps (aligned so that each ends on an adaptation step) are captured once
+  // as a hipGraph and replayed; the head (steps 2..adaptint) and the tail run as plain launches.
+  int64_t p_max = 0;
+  for (size_t c = 0; c < n; ++c) p_max = std::max<int64_t>(p_max, npar[c]);
+  p.lds_matrix = p_max * p_max * (int64_t)sizeof(double) <= 150 * 1024 ? p_max * p_max * (int64_t)sizeof(double) : 0;
+  const int64_t ai = opt->adaptint;
+  int64_t next = 2;  // next step number to enqueue
+  auto plain = [&](int64_t upto) {  // steps next .. upto
+    for (; next <= upto && rc == TCI_OK; ++next) rc = enqueue_step(ctx, st, p, s, ai > 0 && next % ai == 0);
+  };
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
-  if (blocks > 0) {
+  const int64_t G = ai > 0 ? ai : 50;
+  if (ai > 0) plain(std::min<int64_t>(ai, opt->n_steps));  // head: up to the first adaptation step
+  const int64_t blocks = (opt->n_steps - next + 1) / G;
+  if (rc == TCI_OK && blocks > 0) {
     TCI_HIP(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     int crc = TCI_OK;
-    for (int64_t k = 0; k < G && crc == TCI_OK; ++k) crc = enqueue_step(ctx, st, p, s);
+    for (int64_t k = 0; k < G && crc == TCI_OK; ++k) crc = enqueue_step(ctx, st, p, s, ai > 0 && k == G - 1);
     hipError_t ce = hipStreamEndCapture(s, &graph);
     if (crc != TCI_OK || ce != hipSuccess) {
       if (graph) (void)hipGraphDestroy(graph);
@@ -651,8 +662,9 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
       return hip_fail(ctx, e, "hipGraphInstantiate");
     }
     for (int64_t b = 0; b < blocks && e == hipSuccess; ++b) e = hipGraphLaunch(exec, s);
+    next += blocks * G;
   }
-  for (int64_t k = 0; k < rest && rc == TCI_OK && e == hipSuccess; ++k) rc = enqueue_step(ctx, st, p, s);
+  if (e == hipSuccess) plain(opt->n_steps);  // tail
   const hipError_t ge = e;
   TCI_HIP(ctx, hipEventRecord(ev1, s));
   TCI_HIP(ctx, hipStreamSynchronize(s));

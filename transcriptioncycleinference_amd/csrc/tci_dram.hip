@@ -34,8 +34,6 @@ namespace tci {
 
 namespace {
 
-constexpr int kWaves = 4;
-
 enum Purpose : uint32_t { P_NORM1 = 1, P_U1 = 2, P_NORM2 = 3, P_U2 = 4, P_GAMMA = 5 };
 
 __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
@@ -103,105 +101,134 @@ __device__ __forceinline__ double wsum64(double x) {
   return x;
 }
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+constexpr int kThreads = 256;  // one workgroup (4 waves) per chain
+constexpr int kVec = TCI_MAX_POINTS + 8;
+
+// Workgroup sum (all threads get the result). red: LDS scratch of >= 4 doubles.
+__device__ double block_sum(double x, double* red) {
+  x = wsum64(x);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = x;
+  __syncthreads();
+  const double s = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return s;
 }
 
 // prior SS: sum(((th - mu) ./ sig).^2) (mcmcstat default priorfun)
-__device__ double prior_ss(const double* th, const double* mu, const double* sig, int P, int lane) {
+__device__ double prior_ss(const double* th, const double* mu, const double* sig, int P, double* red) {
   double s = 0.0;
-  for (int j = lane; j < P; j += 64) {
+  for (int j = threadIdx.x; j < P; j += kThreads) {
     const double sg = sig[j];
     if (isfinite(sg)) {
       const double z = (th[j] - mu[j]) / sg;
       s += z * z;
     }
   }
-  return wsum64(s);
+  return block_sum(s, red);
 }
 
-// Column j of the row-vector product (v * M)_j = sum_{i<=j} v_i M[i][j] for an upper-triangular
-// row-major M (stride ld), for the 64 columns j0..j0+63 (one per lane). v in LDS. Eight
-// independent loads are issued per round so the L2/MALL latency overlaps (the wave is otherwise
-// latency-bound on one dependent load per term).
-__device__ __forceinline__ double tri_col(const double* v, const double* M, int64_t ld, int j0, int j, int P) {
-  const int imax = (j0 + 63 < P - 1 ? j0 + 63 : P - 1);  // uniform
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  int i = 0;
-  for (; i + 7 <= imax; i += 8) {
-    double r[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) r[u] = (i + u <= j && j < P) ? M[(int64_t)(i + u) * ld + j] : 0.0;
-    a0 = fma(v[i + 0], r[0], a0);
-    a1 = fma(v[i + 1], r[1], a1);
-    a2 = fma(v[i + 2], r[2], a2);
-    a3 = fma(v[i + 3], r[3], a3);
-    a0 = fma(v[i + 4], r[4], a0);
-    a1 = fma(v[i + 5], r[5], a1);
-    a2 = fma(v[i + 6], r[6], a2);
-    a3 = fma(v[i + 7], r[7], a3);
-  }
-  for (; i <= imax; ++i)
-    if (i <= j && j < P) a0 = fma(v[i], M[(int64_t)i * ld + j], a0);
-  return (a0 + a1) + (a2 + a3);
-}
-
-// out[j] = base[j] + scale * sum_i z_i R[i][j] (R upper triangular, row-major ld); returns whether
-// every out[j] is inside [lo, hi]. z in LDS.
-__device__ bool propose(const double* base, const double* R, int64_t ld, const double* z, double scale, int P,
-                        const double* lo, const double* hi, double* out, int lane) {
-  bool inb = true;
+// Row-vector times upper-triangular matrix, out_j = sum_{i<=j} v_i M[i][j] (M row-major, stride
+// ld, in global memory), for up to two vectors sharing each load of M. Wave w takes the rows
+// i == w (mod 4) (balanced over the triangle); lanes take columns; 8 loads in flight per lane.
+// v0/v1 and the outputs are in LDS; part = LDS [2][4][kVec].
+template <int NV>
+__device__ void tri_vecmat(const double* v0, const double* v1, const double* M, int64_t ld, int P, double* part,
+                           double* out0, double* out1) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int j0 = 0; j0 < P; j0 += 64) {
     const int j = j0 + lane;
-    const double acc = tri_col(z, R, ld, j0, j, P);
+    const int imax = (j0 + 63 < P - 1 ? j0 + 63 : P - 1);  // uniform
+    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+    int i = w;
+    for (; i + 28 <= imax; i += 32) {
+      double r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int ii = i + 4 * u;
+        r[u] = (ii <= j && j < P) ? M[(int64_t)ii * ld + j] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        a0 = fma(v0[i + 4 * u], r[u], a0);
+        a1 = fma(v0[i + 4 * u + 4], r[u + 1], a1);
+        if (NV == 2) {
+          b0 = fma(v1[i + 4 * u], r[u], b0);
+          b1 = fma(v1[i + 4 * u + 4], r[u + 1], b1);
+        }
+      }
+    }
+    for (; i <= imax; i += 4) {
+      const double r = (i <= j && j < P) ? M[(int64_t)i * ld + j] : 0.0;
+      a0 = fma(v0[i], r, a0);
+      if (NV == 2) b0 = fma(v1[i], r, b0);
+    }
     if (j < P) {
-      const double v = base[j] + scale * acc;
-      out[j] = v;
-      inb = inb && v >= lo[j] && v <= hi[j];
+      part[(0 * 4 + w) * kVec + j] = a0 + a1;
+      if (NV == 2) part[(1 * 4 + w) * kVec + j] = b0 + b1;
     }
   }
-  return __all(inb);
-}
-
-// |d * iR|^2 with d = a - b (row vector), iR upper triangular.
-__device__ double mahal(const double* a, const double* b, const double* iR, int64_t ld, int P, double* dl, int lane) {
-  for (int j = lane; j < P; j += 64) dl[j] = a[j] - b[j];
-  wave_sync();
-  double s = 0.0;
-  for (int j0 = 0; j0 < P; j0 += 64) {
-    const int j = j0 + lane;
-    const double acc = tri_col(dl, iR, ld, j0, j, P);
-    if (j < P) s += acc * acc;
+  __syncthreads();
+  for (int j = threadIdx.x; j < P; j += kThreads) {
+    out0[j] = (part[0 * kVec + j] + part[1 * kVec + j]) + (part[2 * kVec + j] + part[3 * kVec + j]);
+    if (NV == 2)
+      out1[j] = (part[4 * kVec + j] + part[5 * kVec + j]) + (part[6 * kVec + j] + part[7 * kVec + j]);
   }
-  wave_sync();
-  return wsum64(s);
+  __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void k_init(DramState st, const double* __restrict__ qdiag,
-                                              const double* __restrict__ s2_0) {
-  const int lane = threadIdx.x & 63;
-  const int64_t c = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+struct Smem {
+  double z[kVec];
+  double y[kVec];
+  double d0[kVec];
+  double d1[kVec];
+  double part[8 * kVec];
+  double red[8];
+  int flag;
+};
+
+// Draw z (stream `purpose`), y = base + scale * z*R into LDS and global `out`; returns in-bounds.
+__device__ bool propose_block(const DramState& st, const DramParams& p, int64_t c, int64_t step, uint32_t purpose,
+                              const double* base, double scale, int P, double* out, Smem& sm) {
+  const int64_t ld = st.ld;
+  for (int j = threadIdx.x; j < P; j += kThreads) sm.z[j] = normal_at(p.seed, c, step, purpose, j);
+  __syncthreads();
+  tri_vecmat<1>(sm.z, nullptr, st.R + c * ld * ld, ld, P, sm.part, sm.y, nullptr);
+  int inb = 1;
+  for (int j = threadIdx.x; j < P; j += kThreads) {
+    const double v = base[j] + scale * sm.y[j];
+    out[j] = v;
+    sm.y[j] = v;
+    inb &= (v >= st.lower[c * ld + j] && v <= st.upper[c * ld + j]) ? 1 : 0;
+  }
+  return __syncthreads_and(inb) != 0;
+}
+
+__global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* __restrict__ qdiag,
+                                                   const double* __restrict__ s2_0) {
+  __shared__ double red[8];
+  const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   double* R = st.R + c * ld * ld;
   double* iR = st.iR + c * ld * ld;
   double* cv = st.cov + c * ld * ld;
-  for (int64_t e = lane; e < ld * ld; e += 64) {
+  for (int64_t e = threadIdx.x; e < ld * ld; e += kThreads) {
     R[e] = 0.0;
     iR[e] = 0.0;
     cv[e] = 0.0;
   }
-  for (int j = lane; j < P; j += 64) {
+  __syncthreads();
+  for (int j = threadIdx.x; j < P; j += kThreads) {
     const double sd = sqrt(qdiag[c * ld + j]);  // R = chol(qcov), qcov = J0 diagonal (:230)
     R[(int64_t)j * ld + j] = sd;
     iR[(int64_t)j * ld + j] = 1.0 / sd;
     st.cmean[c * ld + j] = 0.0;
   }
-  const double pr = prior_ss(st.theta + c * ld, st.pmu + c * ld, st.psig + c * ld, P, lane);
-  if (lane == 0) {
+  const double pr = prior_ss(st.theta + c * ld, st.pmu + c * ld, st.psig + c * ld, P, red);
+  if (threadIdx.x == 0) {
     st.prior[c] = pr;
     st.sigma2[c] = s2_0[c];
     st.wsum[c] = 0.0;
@@ -211,17 +238,18 @@ __global__ __launch_bounds__(256) void k_init(DramState st, const double* __rest
   }
 }
 
-// Row 1 of the chain (the initial state): window, stats, thinned output.
-__device__ void record_row(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P, int lane) {
+// Chain row `row` (1-based) = the current state: covupd window, posterior stats, thinned output.
+__device__ void record_row(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P) {
   const int64_t ld = st.ld;
   const double* th = st.theta + c * ld;
+  const int t = threadIdx.x;
   if (p.adaptint > 0) {
     double* w = st.window + (c * p.adaptint + (row - 1) % p.adaptint) * ld;
-    for (int j = lane; j < P; j += 64) w[j] = th[j];
+    for (int j = t; j < P; j += kThreads) w[j] = th[j];
   }
   if (row >= p.stats_from) {  // posterior mean / population std over chain(stats_from:end, :) (:276-301)
     const double n = (double)(row - p.stats_from + 1);
-    for (int j = lane; j < P; j += 64) {
+    for (int j = t; j < P; j += kThreads) {
       const double x = th[j];
       double m = st.smean[c * ld + j];
       const double d = x - m;
@@ -230,7 +258,7 @@ __device__ void record_row(const DramState& st, const DramParams& p, int64_t c, 
       st.sm2[c * ld + j] += d * (x - m);
     }
   }
-  if (lane == 0) {  // s2 statistics over the whole s2chain (:302-303)
+  if (t == 0) {  // s2 statistics over the whole s2chain (:302-303)
     const double s2 = st.sigma2[c];
     st.s2sum[c] += s2;
     const double q = sqrt(s2), n = (double)row;
@@ -241,54 +269,46 @@ __device__ void record_row(const DramState& st, const DramParams& p, int64_t c, 
   if (st.chain_out != nullptr && p.thin > 0 && (row - 1) % p.thin == 0) {
     const int64_t k = (row - 1) / p.thin;
     if (k < p.n_keep) {
-      for (int j = lane; j < P; j += 64) st.chain_out[(k * st.n_chains + c) * ld + j] = th[j];
-      if (lane == 0 && st.s2_out) st.s2_out[k * st.n_chains + c] = st.sigma2[c];
+      for (int j = t; j < P; j += kThreads) st.chain_out[(k * st.n_chains + c) * ld + j] = th[j];
+      if (t == 0 && st.s2_out) st.s2_out[k * st.n_chains + c] = st.sigma2[c];
     }
   }
 }
 
-__global__ __launch_bounds__(256) void k_init_stats(DramState st, DramParams p) {
-  const int lane = threadIdx.x & 63;
-  const int64_t c = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+__global__ __launch_bounds__(kThreads) void k_init_stats(DramState st, DramParams p) {
+  const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int P = st.npar[c];
-  for (int j = lane; j < P; j += 64) {
+  for (int j = threadIdx.x; j < P; j += kThreads) {
     st.smean[c * st.ld + j] = 0.0;
     st.sm2[c * st.ld + j] = 0.0;
   }
-  if (lane == 0) {
+  if (threadIdx.x == 0) {
     st.s2sum[c] = 0.0;
     st.sq_mean[c] = 0.0;
     st.sq_m2[c] = 0.0;
   }
-  wave_sync();
-  record_row(st, p, c, 1, P, lane);
+  __syncthreads();
+  record_row(st, p, c, 1, P);
 }
 
-__global__ __launch_bounds__(256) void k_propose1(DramState st, DramParams p) {
-  __shared__ double zs[kWaves][TCI_MAX_POINTS + 8];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int64_t c = (int64_t)blockIdx.x * kWaves + w;
+__global__ __launch_bounds__(kThreads) void k_propose1(DramState st, DramParams p) {
+  __shared__ Smem sm;
+  const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int64_t step = *st.step;
   const int64_t ld = st.ld;
   const int P = st.npar[c];
-  for (int j = lane; j < P; j += 64) zs[w][j] = normal_at(p.seed, c, step, P_NORM1, j);
-  wave_sync();
-  const bool inb = propose(st.theta + c * ld, st.R + c * ld * ld, ld, zs[w], 1.0, P, st.lower + c * ld,
-                           st.upper + c * ld, st.prop1 + c * ld, lane);
-  if (lane == 0) {
+  const bool inb = propose_block(st, p, c, step, P_NORM1, st.theta + c * ld, 1.0, P, st.prop1 + c * ld, sm);
+  if (threadIdx.x == 0) {
     st.act1[c] = inb ? 1 : 0;
     if (inb) st.nevals[c] += 1;
   }
 }
 
-__global__ __launch_bounds__(256) void k_accept1(DramState st, DramParams p) {
-  __shared__ double zs[kWaves][TCI_MAX_POINTS + 8];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int64_t c = (int64_t)blockIdx.x * kWaves + w;
+__global__ __launch_bounds__(kThreads) void k_accept1(DramState st, DramParams p) {
+  __shared__ Smem sm;
+  const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int64_t step = *st.step;
   const int64_t ld = st.ld;
@@ -299,42 +319,35 @@ __global__ __launch_bounds__(256) void k_accept1(DramState st, DramParams p) {
   double a12 = 0.0, pr1 = 0.0;
   bool acc = false;
   if (inb) {
-    pr1 = prior_ss(y1, st.pmu + c * ld, st.psig + c * ld, P, lane);
+    pr1 = prior_ss(y1, st.pmu + c * ld, st.psig + c * ld, P, sm.red);
     const double e = -0.5 * (st.ss1[c] - st.ss[c]) / st.sigma2[c] - 0.5 * (pr1 - st.prior[c]);
     a12 = fmin(1.0, exp(e));
     acc = uniform_at(p.seed, c, step, P_U1) < a12;
   }
   if (acc) {
-    for (int j = lane; j < P; j += 64) th[j] = y1[j];
-    if (lane == 0) {
+    for (int j = threadIdx.x; j < P; j += kThreads) th[j] = y1[j];
+    if (threadIdx.x == 0) {
       st.ss[c] = st.ss1[c];
       st.prior[c] = pr1;
       st.naccept[c] += 1;
     }
   }
-  if (lane == 0) {
+  __syncthreads();
+  bool inb2 = false;
+  if (!acc && p.ntry >= 2)  // delayed rejection: second try with R / drscale
+    inb2 = propose_block(st, p, c, step, P_NORM2, th, 1.0 / p.drscale, P, st.prop2 + c * ld, sm);
+  if (threadIdx.x == 0) {
     st.a12[c] = a12;
     st.prior1[c] = pr1;
-  }
-  bool inb2 = false;
-  if (!acc && p.ntry >= 2) {  // delayed rejection: second try with R / drscale
-    for (int j = lane; j < P; j += 64) zs[w][j] = normal_at(p.seed, c, step, P_NORM2, j);
-    wave_sync();
-    inb2 = propose(th, st.R + c * ld * ld, ld, zs[w], 1.0 / p.drscale, P, st.lower + c * ld, st.upper + c * ld,
-                   st.prop2 + c * ld, lane);
-  }
-  if (lane == 0) {
     st.acc1[c] = acc ? 1 : 0;
     st.act2[c] = inb2 ? 1 : 0;
     if (inb2) st.nevals[c] += 1;
   }
 }
 
-__global__ __launch_bounds__(256) void k_accept2(DramState st, DramParams p) {
-  __shared__ double dl[kWaves][TCI_MAX_POINTS + 8];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int64_t c = (int64_t)blockIdx.x * kWaves + w;
+__global__ __launch_bounds__(kThreads) void k_accept2(DramState st, DramParams p) {
+  __shared__ Smem sm;
+  const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int64_t step = *st.step;
   const int64_t ld = st.ld;
@@ -344,85 +357,106 @@ __global__ __launch_bounds__(256) void k_accept2(DramState st, DramParams p) {
   if (p.ntry >= 2 && st.act2[c] != 0) {  // stage 2 was proposed (stage 1 rejected) and is in bounds
     const double* y1 = st.prop1 + c * ld;
     const double* y2 = st.prop2 + c * ld;
-    const double pr2 = prior_ss(y2, st.pmu + c * ld, st.psig + c * ld, P, lane);
+    const double pr2 = prior_ss(y2, st.pmu + c * ld, st.psig + c * ld, P, sm.red);
     const double s2 = st.sigma2[c], ss2 = st.ss2[c], ss1 = st.ss1[c], a12 = st.a12[c];
     // ss1 = +Inf (stage 1 out of bounds) gives alpha32 = 0, alpha12 = 0
     const double a32 = fmin(1.0, exp(-0.5 * (ss1 - ss2) / s2 - 0.5 * (st.prior1[c] - pr2)));
     const double l2 = exp(-0.5 * (ss2 - st.ss[c]) / s2 - 0.5 * (pr2 - st.prior[c]));
-    const double* iR = st.iR + c * ld * ld;
-    const double m21 = mahal(y2, y1, iR, ld, P, dl[w], lane);
-    const double m01 = mahal(th, y1, iR, ld, P, dl[w], lane);
-    const double q1 = exp(-0.5 * (m21 - m01));
+    for (int j = threadIdx.x; j < P; j += kThreads) {
+      sm.d1[j] = y2[j] - y1[j];
+      sm.d0[j] = th[j] - y1[j];
+    }
+    __syncthreads();
+    tri_vecmat<2>(sm.d1, sm.d0, st.iR + c * ld * ld, ld, P, sm.part, sm.z, sm.y);
+    double q21 = 0.0, q01 = 0.0;
+    for (int j = threadIdx.x; j < P; j += kThreads) {
+      q21 += sm.z[j] * sm.z[j];
+      q01 += sm.y[j] * sm.y[j];
+    }
+    q21 = block_sum(q21, sm.red);
+    q01 = block_sum(q01, sm.red);
+    const double q1 = exp(-0.5 * (q21 - q01));  // |(y2-y1) iR|^2 - |(x-y1) iR|^2
     const double a13 = l2 * q1 * (1.0 - a32) / (1.0 - a12);
     acc2 = uniform_at(p.seed, c, step, P_U2) < a13;
     if (acc2) {
-      for (int j = lane; j < P; j += 64) th[j] = y2[j];
-      if (lane == 0) {
+      for (int j = threadIdx.x; j < P; j += kThreads) th[j] = y2[j];
+      if (threadIdx.x == 0) {
         st.ss[c] = ss2;
         st.prior[c] = pr2;
         st.naccept[c] += 1;
       }
     }
   }
-  if (lane == 0 && !(st.acc1[c] != 0 || acc2)) st.nrej_win[c] += 1;  // no stage moved the chain
-  // sigma2 Gibbs update (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/oldss)
-  if (p.updatesigma && lane == 0) {
-    const double a = 0.5 * (double)st.nobs[c];
-    st.sigma2[c] = 1.0 / gamma_at(p.seed, c, step, a, 2.0 / st.ss[c]);
+  if (threadIdx.x == 0) {
+    if (!(st.acc1[c] != 0 || acc2)) st.nrej_win[c] += 1;  // no stage moved the chain
+    // sigma2 Gibbs update (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/oldss)
+    if (p.updatesigma) st.sigma2[c] = 1.0 / gamma_at(p.seed, c, step, 0.5 * (double)st.nobs[c], 2.0 / st.ss[c]);
   }
-  wave_sync();
-  record_row(st, p, c, step, P, lane);
+  __syncthreads();
+  record_row(st, p, c, step, P);
 }
 
 __global__ void k_step_incr(int64_t* step) {
   if (threadIdx.x == 0) *step += 1;
 }
 
-// Adaptation (one 256-thread workgroup per chain).
-__global__ __launch_bounds__(256) void k_adapt(DramState st, DramParams p) {
+// Adaptation, one workgroup per chain (launched only at steps that are multiples of adaptint).
+// Matrices live in LDS when P*P*8 bytes fit (every TestData cell: P <= 136), else in global.
+__global__ __launch_bounds__(kThreads) void k_adapt(DramState st, DramParams p) {
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  __shared__ double xs[kVec];
+  __shared__ double dm[kVec];
+  __shared__ int fail;
   const int t = threadIdx.x;
   const int64_t c = blockIdx.x;
   const int64_t step = *st.step;
   if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
-  double* work = st.work;
   const int64_t ld = st.ld;
   const int P = st.npar[c];
-  double* cv = st.cov + c * ld * ld;
+  double* cvg = st.cov + c * ld * ld;
   double* mu = st.cmean + c * ld;
   double* R = st.R + c * ld * ld;
   double* iR = st.iR + c * ld * ld;
-  double* A = work + c * ld * ld;
-  __shared__ double xs[TCI_MAX_POINTS + 8];
-  __shared__ double dm[TCI_MAX_POINTS + 8];
-  __shared__ int fail;
+  const bool in_lds = p.lds_matrix != 0;
+  double* A = in_lds ? dyn : st.work + c * ld * ld;
+  const int64_t lda = in_lds ? P : ld;
   // ---- covupd: fold the window rows (chain rows step-adaptint+1 .. step) into (mean, cov, wsum)
-  const int64_t nrows = p.adaptint;
+  for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
+    const int i = (int)(e / P), j = (int)(e % P);
+    if (j >= i) A[(int64_t)i * lda + j] = cvg[(int64_t)i * ld + j];
+  }
   double ws = st.wsum[c];
-  for (int64_t r = 0; r < nrows; ++r) {
+  __syncthreads();
+  for (int64_t r = 0; r < p.adaptint; ++r) {
     const double* x = st.window + (c * p.adaptint + r) * ld;
-    for (int j = t; j < P; j += 256) xs[j] = x[j];
+    for (int j = t; j < P; j += kThreads) xs[j] = x[j];
     __syncthreads();
     if (ws == 0.0) {  // first row: mean = x, cov = 0
-      for (int j = t; j < P; j += 256) mu[j] = xs[j];
+      for (int j = t; j < P; j += kThreads) mu[j] = xs[j];
       __syncthreads();
       ws = 1.0;
       continue;
     }
-    for (int j = t; j < P; j += 256) dm[j] = xs[j] - mu[j];
+    for (int j = t; j < P; j += kThreads) dm[j] = xs[j] - mu[j];
     __syncthreads();
     // xcov = oldcov + w/(w+oldwsum-1) * (oldwsum/(w+oldwsum) * d'd - oldcov), w = 1
     const double f1 = 1.0 / ws, f2 = ws / (ws + 1.0);
-    for (int64_t e = t; e < (int64_t)P * P; e += 256) {
+    for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
       const int i = (int)(e / P), j = (int)(e % P);
       if (j < i) continue;
-      const double old = cv[(int64_t)i * ld + j];
-      cv[(int64_t)i * ld + j] = old + f1 * (f2 * dm[i] * dm[j] - old);
+      const double old = A[(int64_t)i * lda + j];
+      A[(int64_t)i * lda + j] = old + f1 * (f2 * dm[i] * dm[j] - old);
     }
-    for (int j = t; j < P; j += 256) mu[j] = mu[j] + dm[j] / (ws + 1.0);
+    for (int j = t; j < P; j += kThreads) mu[j] = mu[j] + dm[j] / (ws + 1.0);
     ws += 1.0;
     __syncthreads();
   }
+  for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
+    const int i = (int)(e / P), j = (int)(e % P);
+    if (j >= i) cvg[(int64_t)i * ld + j] = A[(int64_t)i * lda + j];
+  }
   if (t == 0) st.wsum[c] = ws;
+  __syncthreads();  // the copy-back must read A before the Cholesky below modifies it
   if (step < p.burnintime) {
     // burn-in: no covariance adaptation, only scaling by the window's rejection rate
     const double rate = (double)st.nrej_win[c] / (double)p.adaptint;
@@ -430,7 +464,7 @@ __global__ __launch_bounds__(256) void k_adapt(DramState st, DramParams p) {
     if (rate > 0.95) s = 1.0 / p.burnin_scale;
     else if (rate < 0.05) s = p.burnin_scale;
     if (s != 1.0) {
-      for (int64_t e = t; e < (int64_t)P * P; e += 256) {
+      for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
         const int i = (int)(e / P), j = (int)(e % P);
         R[(int64_t)i * ld + j] *= s;
         iR[(int64_t)i * ld + j] /= s;
@@ -440,51 +474,53 @@ __global__ __launch_bounds__(256) void k_adapt(DramState st, DramParams p) {
     if (t == 0) st.nrej_win[c] = 0;
     return;
   }
-  // ---- R = chol(cov + qcovadj*I) * adascale (upper, A = R'R), then iR = inv(R)
-  for (int64_t e = t; e < (int64_t)P * P; e += 256) {
-    const int i = (int)(e / P), j = (int)(e % P);
-    A[(int64_t)i * ld + j] = j >= i ? cv[(int64_t)i * ld + j] + (i == j ? p.qcovadj : 0.0) : 0.0;
-  }
+  // ---- R = chol(cov + qcovadj*I) * adascale (upper, A = R'R), in place on A
+  for (int i = t; i < P; i += kThreads) A[(int64_t)i * lda + i] += p.qcovadj;
   if (t == 0) fail = 0;
   __syncthreads();
   for (int k = 0; k < P; ++k) {
     if (t == 0) {
-      const double d = A[(int64_t)k * ld + k];
+      const double d = A[(int64_t)k * lda + k];
       if (!(d > 0.0) || !isfinite(d)) fail = 1;
-      A[(int64_t)k * ld + k] = sqrt(d);
+      A[(int64_t)k * lda + k] = sqrt(d);
     }
     __syncthreads();
     if (fail) break;
-    const double dk = A[(int64_t)k * ld + k];
-    for (int j = k + 1 + t; j < P; j += 256) A[(int64_t)k * ld + j] /= dk;
+    const double dk = A[(int64_t)k * lda + k];
+    for (int j = k + 1 + t; j < P; j += kThreads) A[(int64_t)k * lda + j] /= dk;
     __syncthreads();
     const int m = P - k - 1;
-    for (int64_t e = t; e < (int64_t)m * m; e += 256) {
+    for (int64_t e = t; e < (int64_t)m * m; e += kThreads) {
       const int i = k + 1 + (int)(e / m), j = k + 1 + (int)(e % m);
-      if (j >= i) A[(int64_t)i * ld + j] -= A[(int64_t)k * ld + i] * A[(int64_t)k * ld + j];
+      if (j >= i) A[(int64_t)i * lda + j] -= A[(int64_t)k * lda + i] * A[(int64_t)k * lda + j];
     }
     __syncthreads();
   }
   if (!fail) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
-    for (int64_t e = t; e < (int64_t)P * P; e += 256) {
+    for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
       const int i = (int)(e / P), j = (int)(e % P);
-      R[(int64_t)i * ld + j] = j >= i ? A[(int64_t)i * ld + j] * sc : 0.0;
+      const double r = j >= i ? A[(int64_t)i * lda + j] * sc : 0.0;
+      A[(int64_t)i * lda + j] = r;  // A now holds R (upper), lower part zero
+      R[(int64_t)i * ld + j] = r;
     }
     __syncthreads();
-    // iR = R \ I : column j by back substitution (one thread per column)
-    for (int j = t; j < P; j += 256) {
-      for (int i = P - 1; i >= 0; --i) {
-        double v;
-        if (i > j) {
-          v = 0.0;
-        } else {
-          double s = i == j ? 1.0 : 0.0;
-          for (int k = i + 1; k <= j; ++k) s -= R[(int64_t)i * ld + k] * iR[(int64_t)k * ld + j];
-          v = s / R[(int64_t)i * ld + i];
-        }
-        iR[(int64_t)i * ld + j] = v;
+    // iR = R \ I, in place on A, row by row from the bottom: X(i,j) = (d_ij - sum_{k=i+1..j} R(i,k) X(k,j)) / R(i,i)
+    for (int i = P - 1; i >= 0; --i) {
+      const double rii = A[(int64_t)i * lda + i];
+      // row i of R (k > i) is read before being overwritten by row i of X: stage it
+      for (int k = i + 1 + t; k < P; k += kThreads) xs[k] = A[(int64_t)i * lda + k];
+      __syncthreads();
+      for (int j = i + t; j < P; j += kThreads) {
+        double s = (i == j) ? 1.0 : 0.0;
+        for (int k = i + 1; k <= j; ++k) s -= xs[k] * A[(int64_t)k * lda + j];
+        A[(int64_t)i * lda + j] = s / rii;
       }
+      __syncthreads();
+    }
+    for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
+      const int i = (int)(e / P), j = (int)(e % P);
+      iR[(int64_t)i * ld + j] = j >= i ? A[(int64_t)i * lda + j] : 0.0;
     }
   }
   __syncthreads();
@@ -492,32 +528,36 @@ __global__ __launch_bounds__(256) void k_adapt(DramState st, DramParams p) {
 }
 
 inline int finish() { return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP; }
-inline dim3 wave_grid(int64_t n) { return dim3((unsigned)((n + kWaves - 1) / kWaves)); }
+inline dim3 chain_grid(int64_t n) { return dim3((unsigned)n); }
 
 }  // namespace
 
 int dram_launch_init(const DramState& st, const double* qcov_diag, const double* sigma2_0, void* stream) {
-  hipLaunchKernelGGL(k_init, wave_grid(st.n_chains), dim3(256), 0, (hipStream_t)stream, st, qcov_diag, sigma2_0);
+  hipLaunchKernelGGL(k_init, chain_grid(st.n_chains), dim3(kThreads), 0, (hipStream_t)stream, st, qcov_diag, sigma2_0);
   return finish();
 }
 int dram_launch_init_stats(const DramState& st, const DramParams& p, void* stream) {
-  hipLaunchKernelGGL(k_init_stats, wave_grid(st.n_chains), dim3(256), 0, (hipStream_t)stream, st, p);
+  hipLaunchKernelGGL(k_init_stats, chain_grid(st.n_chains), dim3(kThreads), 0, (hipStream_t)stream, st, p);
   return finish();
 }
 int dram_launch_propose1(const DramState& st, const DramParams& p, void* stream) {
-  hipLaunchKernelGGL(k_propose1, wave_grid(st.n_chains), dim3(256), 0, (hipStream_t)stream, st, p);
+  hipLaunchKernelGGL(k_propose1, chain_grid(st.n_chains), dim3(kThreads), 0, (hipStream_t)stream, st, p);
   return finish();
 }
 int dram_launch_accept1(const DramState& st, const DramParams& p, void* stream) {
-  hipLaunchKernelGGL(k_accept1, wave_grid(st.n_chains), dim3(256), 0, (hipStream_t)stream, st, p);
+  hipLaunchKernelGGL(k_accept1, chain_grid(st.n_chains), dim3(kThreads), 0, (hipStream_t)stream, st, p);
   return finish();
 }
 int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream) {
-  hipLaunchKernelGGL(k_accept2, wave_grid(st.n_chains), dim3(256), 0, (hipStream_t)stream, st, p);
+  hipLaunchKernelGGL(k_accept2, chain_grid(st.n_chains), dim3(kThreads), 0, (hipStream_t)stream, st, p);
   return finish();
 }
 int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
-  hipLaunchKernelGGL(k_adapt, dim3((unsigned)st.n_chains), dim3(256), 0, (hipStream_t)stream, st, p);
+  const size_t lds = p.lds_matrix ? (size_t)p.lds_matrix : 0;
+  if (lds > 0 && hipFuncSetAttribute((const void*)k_adapt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+                     hipSuccess)
+    return TCI_EHIP;
+  hipLaunchKernelGGL(k_adapt, chain_grid(st.n_chains), dim3(kThreads), lds, (hipStream_t)stream, st, p);
   return finish();
 }
 int dram_launch_step_incr(const DramState& st, void* stream) {

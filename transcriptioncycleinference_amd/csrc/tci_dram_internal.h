@@ -7,7 +7,7 @@
 
 namespace tci {
 
-// All arrays are indexed by chain c; vectors have stride ld (= max parameter count P_max),
+// One workgroup (256 threads) per chain. All arrays are indexed by chain c; vectors have stride ld (= max parameter count P_max),
 // matrices stride ld*ld (row-major, P_c x P_c used).
 struct DramState {
   int64_t n_chains;
@@ -65,6 +65,7 @@ struct DramParams {
   int64_t stats_from;
   int64_t thin;
   int64_t n_keep;
+  int64_t lds_matrix;  // bytes of dynamic LDS for the adaptation matrix (0 = work in global memory)
 };
 
 int dram_launch_init(const DramState& st, const double* qcov_diag, const double* sigma2_0, void* stream);
