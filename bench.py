@@ -117,6 +117,21 @@ def cpu_baseline(cells, theta, cid, active, seconds: float):
                       f"OpenMP {threads} threads"}
 
 
+def end_to_end(lk, n_steps: int):
+    """SURVEY §8(d) mode (ii): the reference's whole fit -- one DRAM chain per TestData cell,
+    n_steps (200k) steps, n_burn = n_steps/20, GPU-resident sampler; every ssfun call is the
+    batched kernel. Reported beside `value` (a step there is one batched launch)."""
+    from transcriptioncycleinference_amd.mcmc import fit
+
+    t0 = time.perf_counter()
+    fr = fit(lk, n_steps=n_steps, n_burn=max(1, n_steps // 20), seed=1)
+    wall = time.perf_counter() - t0
+    return {"n_steps": n_steps, "chains": len(fr.MCMCresults), "device_s": fr.elapsed_ms * 1e-3, "wall_s": wall,
+            "ssfun_evals": fr.n_evals, "value": fr.n_evals / (fr.elapsed_ms * 1e-3), "unit": "SS evals/s",
+            "us_per_step": fr.elapsed_ms * 1e3 / max(n_steps - 1, 1),
+            "accept_rate_median": float(np.median(fr.accept_rate))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -125,6 +140,8 @@ def main():
     ap.add_argument("--proposals", type=int, default=256, help="DRAM-style proposals per cell per launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dram-steps", type=int, default=200000,
+                    help="end-to-end mode: one DRAM chain per TestData cell for this many steps (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -253,6 +270,8 @@ def main():
         res["host_api_pcie_inclusive"] = {"value": n_active / h_el, "unit": "SS evals/s",
                                           "ms_per_call": h_el * 1e3, "bytes_h2d": int(theta.nbytes + cid.nbytes
                                                                                     + active.nbytes)}
+    if rank == 0 and world == 1 and args.dram_steps > 1:
+        res["end_to_end_dram"] = end_to_end(lk, args.dram_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cells, theta, cid, active, args.cpu_seconds)
     if rank == 0:
