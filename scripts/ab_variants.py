@@ -16,16 +16,14 @@ OUT = os.path.join(ROOT, "build", "ab")
 
 VARIANTS = {
     "ship": [],
-    "w6": ["TCI_WAVES_PER_EU=6"],
+    "abl_rows": ["TCI_ABLATE=1"],
+    "abl_bounds": ["TCI_ABLATE=2"],
+    "abl_interp": ["TCI_ABLATE=4"],
+    "abl_scan": ["TCI_ABLATE=8"],
+    "abl_all": ["TCI_ABLATE=15"],
     "w6_noxcd": ["TCI_WAVES_PER_EU=6", "TCI_XCD_REMAP=0"],
-    "w7": ["TCI_WAVES_PER_EU=7"],
-    "w5": ["TCI_WAVES_PER_EU=5"],
     "w8_latepts": ["TCI_WAVES_PER_EU=8", "TCI_EARLY_POINTS=0"],
-    "w6_latepts_noxcd": ["TCI_WAVES_PER_EU=6", "TCI_EARLY_POINTS=0", "TCI_XCD_REMAP=0"],
-    "noxcd": ["TCI_XCD_REMAP=0"],
     "loopramp": ["TCI_RAMP_PREFIX=0"],
-    "latepts": ["TCI_EARLY_POINTS=0"],
-    "w8": ["TCI_WAVES_PER_EU=8"],
 }
 
 
@@ -70,10 +68,10 @@ def run(names, rounds, launches, proposals):
     res = {}
     for n in names:
         got = outs[n].cpu().numpy()
-        rel = float(np.max(np.abs(got[act] - ref[act]) / np.abs(ref[act])))
+        rel = float(np.nanmax(np.abs(got[act] - ref[act]) / np.abs(ref[act])))
         t = np.array(times[n])
         res[n] = {"median_us": float(np.median(t)), "min_us": float(t.min()), "rel_vs_first": rel,
-                  "evals_per_s": float(act.sum() / (np.median(t) * 1e-6)), "defines": VARIANTS[n]}
+                  "evals_per_s": float(act.sum() / (np.median(t) * 1e-6)), "defines": VARIANTS.get(n)}
     print(json.dumps(res, indent=1))
 
 
@@ -81,7 +79,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--run", action="store_true")
-    ap.add_argument("--variants", default="ship,w6,w6_noxcd,w7,w5,w8_latepts,w6_latepts_noxcd")
+    ap.add_argument("--variants", default="ship,abl_rows,abl_bounds,abl_interp,abl_scan,abl_all")
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--proposals", type=int, default=256)

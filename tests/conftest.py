@@ -10,6 +10,14 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+# Load torch (and its HIP runtime) before libtci.so: both carry the soname libamdhip64.so.7, and
+# whichever loads first serves the process. bench.py imports torch first too.
+try:
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    pass
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
 

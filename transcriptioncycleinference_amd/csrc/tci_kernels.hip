@@ -58,6 +58,9 @@
 #ifndef TCI_EARLY_POINTS
 #define TCI_EARLY_POINTS 1   // issue the acquisition-point loads with the first round trip
 #endif
+#ifndef TCI_ABLATE
+#define TCI_ABLATE 0         // diagnostics only (wrong results): bit0 rows, bit1 bounds, bit2 interp, bit3 scan
+#endif
 #ifndef TCI_WAVES_PER_EU
 #define TCI_WAVES_PER_EU 6   // register budget for 6 waves/SIMD (A/B: 50 us vs 58 us at the
 #endif                       // compiler's default 5 waves; 7-8 waves no faster)
@@ -133,8 +136,9 @@ struct Regions {
 // Exact prefix tables of the fast path, interleaved per cohort index i (LDS, 16 B per entry):
 //   K_i = sum_{i' <= i} c_i'        (= floor(counter_i): polymerases loaded through step i)
 //   J_i = sum_{i' <= i} i' * c_i'
-// Both are integers < 2^53, exact in any summation order. Entry 0 holds i = -1 (zeros).
-__device__ __forceinline__ double2 kj_at(const double2* KJ, int i) { return KJ[(i < -1 ? -1 : i) + 1]; }
+// Both are integers < 2^53, exact in any summation order. KJ points at i = 0 of a table whose
+// SLOTS entries below i = 0 are zeros, so every index r - m - 1 >= -SLOTS needs no clamp.
+__device__ __forceinline__ double2 kj_at(const double2* KJ, int i) { return KJ[i]; }
 
 // Row sum of one segment of one dye on the fast path (see the header), O(1) per row:
 //   full  (e < P_m < L, m in [f_lo, f_hi]):  phi * (K[r - f_lo] - K[r - f_hi - 1])
@@ -180,7 +184,7 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
   constexpr int SLOTS = 64 * RPL;      // rows 1..SLOTS (row 0 never holds a polymerase)
   constexpr int SIMP = SLOTS + 2;      // offset of the PP7 row array
   constexpr int NPT = RPL + 1;         // acquisition points per lane (N <= 64*RPL + 1)
-  constexpr int WAVE_DOUBLES = 2 * SLOTS + 4;  // {K,J} table (SLOTS+1 entries) / the two sim rows
+  constexpr int WAVE_DOUBLES = 4 * SLOTS + 4;  // {K,J} table (2*SLOTS+1 entries) / the two sim rows
   __shared__ __attribute__((aligned(16))) double s_lds[kWavesPerBlock][WAVE_DOUBLES];
 
   const int lane = threadIdx.x & 63;
@@ -251,8 +255,7 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
     const int g = RPL * lane + q;
     const bool valid = g < nsteps;
     fin = fin && (!valid || isfinite(dr[q]));
-    double rho = R + dr[q];
-    rho = rho < 0.0 ? 0.0 : rho;
+    const double rho = fmax(R + dr[q], 0.0);  // R(R<0) = 0 (the sign of a zero cannot reach floor())
     prod[q] = (valid && !(st[q].t < ton)) ? rho * st[q].dt : 0.0;  // skipped steps add nothing (:57-60)
     vd[q] = valid ? v * st[q].dt : 0.0;                              // v*dt(i), rounded once (:64)
   }
@@ -271,14 +274,19 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
       s = s + prod[q];
       loc[q] = s;
     }
+#if TCI_ABLATE & 8
+    const double excl = 0.0;
+#else
     const double excl = wave_shr1(wave_incl_scan(s));
+#endif
     bool amb = false;
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
       const double Sq = excl + loc[q];
       const double eps = Sq * 0x1p-42;  // >> the (g + 16) ulp bound between any two summation orders
-      amb = amb | (floor(Sq - eps) != floor(Sq + eps));
-      K[q] = floor(Sq);
+      const double Kq = floor(Sq);
+      amb = amb | (Sq - eps < Kq) | (Sq + eps >= Kq + 1.0);  // an integer within eps of Sq
+      K[q] = Kq;
     }
     if ((kp.force_exact & 1) || __any(amb)) {
       // Exact path: the reference's serial loop, counter = counter + R(i)*dt(i).
@@ -321,10 +329,23 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
     bool fast = MODE != MODE_FWD_RAW && !(kp.force_exact & 2);
     const double vd0 = v * cm.d;
     Regions rgM[NSEG], rgP[NSEG];
+#if TCI_ABLATE & 2
     if (fast) {
+#pragma unroll
+      for (int k = 0; k < NSEG; ++k) {
+        const int m0 = (int)(sm[k].a / vd0);
+        rgM[k] = Regions{m0 + 1, m0 + 4, m0 + 5, m0 + 20};
+        rgP[k] = Regions{m0 + 9, m0 + 12, m0 + 13, m0 + 20};
+      }
+    }
+    if (false) {
+#else
+    if (fast) {
+#endif
       // ---- distance regions and their exactness proof
-      const double vdl = v * cm.delta;
-      const double vdd = v * (cm.d + cm.delta);
+      // |p(r, r-m) - P_m| <= m*v*delta + (m+3)*u*m*v*(d+delta) <= eps (taken at m = nsteps), doubled
+      const double mx = (double)nsteps;
+      const double eps = 2.0 * (mx * v * cm.delta + (mx + 4.0) * kUnitRoundoff * mx * v * (cm.d + cm.delta));
       bool amb = false;
       int n_lt_L = 0;
       int nM_le_a[NSEG], nM_lt_e[NSEG], nM_le_e[NSEG], nP_le_a[NSEG], nP_lt_e[NSEG], nP_le_e[NSEG];
@@ -336,8 +357,6 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
         const bool valid = g < nsteps;
         const double md = (double)(g + 1);
         const double Pm = md * vd0;
-        // |p(r, r-m) - P_m| <= m*v*delta + (m+3)*u*m*v*(d+delta); doubled for margin
-        const double eps = 2.0 * (md * vdl + (md + 4.0) * kUnitRoundoff * md * vdd);
         bool near = fabs(Pm - L) <= eps;
         n_lt_L += count_true(valid & (Pm < L));
 #pragma unroll
@@ -374,18 +393,26 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
         }
       }
       const double jexcl = wave_shr1(wave_incl_scan(js));
-      double2* KJ = reinterpret_cast<double2*>(lds);
+      double2* KJ = reinterpret_cast<double2*>(lds) + SLOTS + 1;  // KJ[i], i in [-SLOTS-1, SLOTS)
 #pragma unroll
-      for (int q = 0; q < RPL; ++q) KJ[RPL * lane + q + 1] = make_double2(K[q], jexcl + jloc[q]);
-      if (lane == 0) KJ[0] = make_double2(0.0, 0.0);
+      for (int q = 0; q < RPL; ++q) {
+        KJ[RPL * lane + q] = make_double2(K[q], jexcl + jloc[q]);
+        KJ[RPL * lane + q - SLOTS - 1] = make_double2(0.0, 0.0);
+      }
+      if (lane == 0) KJ[-1] = make_double2(0.0, 0.0);
       wave_sync();
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {
         const int r = RPL * lane + q + 1;
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) {
+#if TCI_ABLATE & 1
+          accM[k][q] = KJ[r].x + (double)rgM[k].f_lo;
+          accP[k][q] = KJ[r].y + (double)rgP[k].f_hi;
+#else
           accM[k][q] = row_sum(KJ, r, rgM[k], sm[k], vd0);
           accP[k][q] = row_sum(KJ, r, rgP[k], sp[k], vd0);
+#endif
         }
       }
     } else {
@@ -435,13 +462,12 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
   for (int q = 0; q < RPL; ++q) {
     const int g = RPL * lane + q;
     if (g < nsteps) {
+      // MS2(MS2 < basal) = basal == max(MS2, basal): the sums are finite and >= 0 here
       double m = 0.0, pp = 0.0;
 #pragma unroll
       for (int k = 0; k < NSEG; ++k) {
-        m = m + accM[k][q];
-        m = m < b1 ? b1 : m;
-        pp = pp + accP[k][q];
-        pp = pp < b2 ? b2 : pp;
+        m = fmax(m + accM[k][q], b1);
+        pp = fmax(pp + accP[k][q], b2);
       }
       simM[g + 1] = A * m;
       simP[g + 1] = pp;
@@ -471,6 +497,14 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
   //      squared residuals over [MS2, PP7] (:57-64).
   if (!TCI_EARLY_POINTS) load_points();
   double ss = 0.0;
+#if TCI_ABLATE & 4
+  if (MODE == MODE_SS) {
+    ss = simM[lane] + simP[lane] + pt[0].y1 + pt[1].y2;
+    ss = lane63(wave_incl_scan(ss));
+    if (lane == 0) out0[b] = ss;
+    return;
+  }
+#endif
 #pragma unroll
   for (int kk = 0; kk < NPT; ++kk) {
     if (kk == RPL && N <= 64 * RPL) break;  // uniform: only N = 64*RPL + 1 has a tail point
@@ -480,8 +514,8 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
       double m = NAN, pp = NAN;
       if (k >= 0) {
         const double w = pt[kk].w;
-        m = simM[k] + w * (simM[k + 1] - simM[k]);
-        pp = simP[k] + w * (simP[k + 1] - simP[k]);
+        m = fma(w, simM[k + 1] - simM[k], simM[k]);
+        pp = fma(w, simP[k + 1] - simP[k], simP[k]);
       }
       if (MODE == MODE_FWD_INTERP) {
         out0[b * ld_out + j] = m;
