@@ -40,7 +40,7 @@ def build_library(force: bool = False, verbose: bool = False, out: str = LIB, de
     if out == LIB and not defines and not force and not needs_rebuild():
         return LIB
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wall", "-Wno-bitwise-instead-of-logical", "-I" + os.path.join(REPO_ROOT, "include"), "-I" + CSRC,
+           "-Wall", "-Wno-bitwise-instead-of-logical", "-Wno-pass-failed", "-I" + os.path.join(REPO_ROOT, "include"), "-I" + CSRC,
            *[f"-D{d}" for d in (defines or [])], *SOURCES, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -252,7 +252,7 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
   ctx->stride = stride;
   const size_t total = (size_t)C * (size_t)stride;
   std::vector<tci::StepRec> steps(total, tci::StepRec{0.0, 0.0}), steps_raw(total, tci::StepRec{0.0, 0.0});
-  std::vector<tci::PointRec> points(total, tci::PointRec{0.0, NAN, NAN, -1.0});
+  std::vector<tci::PointRec> points(total, tci::PointRec{NAN, NAN, NAN, 0, 0});
   ctx->grid.assign(total, 0.0);
   for (int64_t c = 0; c < C; ++c) {
     const int64_t o = cells->offsets[c], n = ctx->meta[(size_t)c].n, base = c * stride;
@@ -281,8 +281,13 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
     }
     ctx->meta[(size_t)c].d = dgrid;
     ctx->meta[(size_t)c].delta = delta;
+    // |p(r, r-m) - m*(v*d)| <= v * (m*delta + (m+4)*u*m*(d+delta)) for every distance m <= n-1
+    // (tci_kernels.hip, fast path); doubled, plus 2^-40 relative for the rounding of v * eps_v.
+    const double mx = (double)(n - 1);
+    ctx->meta[(size_t)c].eps_v =
+        2.0 * (mx * delta + (mx + 4.0) * 0x1p-53 * mx * (dgrid + delta)) * (1.0 + 0x1p-40);
     // interp1(t_interp, y, t): interval k = last grid point <= t_j (clamped to n-2);
-    // outside [t_interp(1), t_interp(end)] -> NaN (k = -1).
+    // outside [t_interp(1), t_interp(end)] -> NaN (w = NaN, k = 0).
     for (int64_t j = 0; j < n; ++j) {
       tci::PointRec& pr = points[(size_t)(base + j)];
       pr.y1 = cells->ms2[o + j];
@@ -291,7 +296,7 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
       if (!(q >= g[0] && q <= g[(size_t)n - 1])) continue;
       int64_t k = (int64_t)(std::upper_bound(g.begin(), g.end(), q) - g.begin()) - 1;
       k = std::min(std::max(k, (int64_t)0), n - 2);
-      pr.k = (double)k;
+      pr.k = (int32_t)k;
       pr.w = (q - g[(size_t)k]) / (g[(size_t)k + 1] - g[(size_t)k]);
     }
   }

@@ -15,7 +15,7 @@ struct CellMeta {
   int32_t pad;
   double d;      // grid increment of t(1):d:t(end) (SumofSquares...m:29)
   double delta;  // max_j |(t_interp(j+1) - t_interp(j)) - d| over the grid (a few ulps)
-  double pad2;
+  double eps_v;  // fast-path position bound per unit v (tci_kernels.hip): eps = v * eps_v
 };
 
 // Per grid step g: the step length and the step's start time (ConstantElongationSim.m:43-45,57).
@@ -24,13 +24,15 @@ struct StepRec {
   double t;
 };
 
-// Per acquisition point j: interp1 weight and interval (as a double; -1 = outside the grid,
-// SumofSquares...m:55-56) and the data (NaN = missing).
+// Per acquisition point j: interp1 interval k and weight w (SumofSquares...m:55-56) and the
+// data (NaN = missing). A point outside the grid has w = NaN and k = 0, so its interpolated
+// value is NaN exactly as interp1 returns; padding records (j >= N) are all-NaN.
 struct PointRec {
   double w;
   double y1;  // MS2
   double y2;  // PP7
-  double k;
+  int32_t k;
+  int32_t pad;
 };
 
 // One stem-loop segment of one dye (GetFluorFromPolPos.m:21-27,48-52,60-64).

@@ -74,7 +74,6 @@ namespace tci {
 
 namespace {
 
-constexpr double kUnitRoundoff = 0x1p-53;
 constexpr int kWavesPerBlock = 4;
 
 template <int CTRL, int ROW_MASK>
@@ -113,7 +112,23 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ int count_true(bool p) { return __popcll(__ballot(p)); }
+// Wave votes straight on the compare mask (the int-predicate __ballot/__any/__all round-trip
+// every bool through a VGPR select and a compare: two extra VALU per vote).
+// Votes are OR-ed / AND-ed as 64-bit masks on the scalar unit; the ballot operand is kept a
+// single compare.
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// Mask of the lanes l whose slot RPL*l + q is a loading step (g < nsteps), built on the scalar
+// unit: lanes 0 .. ceil((nsteps - q) / RPL) - 1.
+template <int RPL>
+__device__ __forceinline__ uint64_t step_lanes(int nsteps, int q) {
+  const int n = nsteps > q ? (nsteps - q + RPL - 1) / RPL : 0;
+  return n >= 64 ? ~0ull : (1ull << n) - 1;
+}
+
+// Exponent field of a double: all ones iff the value is +-Inf or NaN. The max over the
+// wave-uniform theta entries stays on the scalar unit (isfinite() would be a vector compare each).
+__device__ __forceinline__ unsigned exp_bits(double x) { return (unsigned)__double2hiint(x) & 0x7ff00000u; }
 
 // Stem-loop occupancy of one polymerase at position p (GetFluorFromPolPos.m:50-52):
 //   phi                 if e < p < L
@@ -235,7 +250,7 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
     for (int k = 0; k < NPT; ++k) {
       const int j = lane + 64 * k;
       if (j <= SLOTS) pt[k] = PT[j];
-      else pt[k] = PointRec{0.0, 0.0, 0.0, -1.0};
+      else pt[k] = PointRec{NAN, NAN, NAN, 0, 0};  // beyond every cell's points: dropped
     }
   };
   if (TCI_EARLY_POINTS && MODE != MODE_FWD_RAW) load_points();
@@ -247,19 +262,20 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
   const int nsteps = N - 1;  // loading steps = rows that can hold polymerases
 
   // ---- per-step setup: R_full = R + dR (SumofSquares...m:45); R<0 -> 0 (ConstantElongationSim.m:36)
-  double vd[RPL], prod[RPL];
-  bool fin = isfinite(v) && isfinite(tau) && isfinite(ton) && isfinite(b1) && isfinite(b2) && isfinite(A) &&
-             isfinite(R);
+  double prod[RPL];
+  const unsigned ebits = max(max(max(exp_bits(v), exp_bits(tau)), max(exp_bits(ton), exp_bits(b1))),
+                            max(max(exp_bits(b2), exp_bits(A)), exp_bits(R)));
+  const bool fin = ebits != 0x7ff00000u;
+  uint64_t nonfinite = 0;
 #pragma unroll
   for (int q = 0; q < RPL; ++q) {
     const int g = RPL * lane + q;
     const bool valid = g < nsteps;
-    fin = fin && (!valid || isfinite(dr[q]));
+    nonfinite |= step_lanes<RPL>(nsteps, q) & wave_ballot(!isfinite(dr[q]));
     const double rho = fmax(R + dr[q], 0.0);  // R(R<0) = 0 (the sign of a zero cannot reach floor())
     prod[q] = (valid && !(st[q].t < ton)) ? rho * st[q].dt : 0.0;  // skipped steps add nothing (:57-60)
-    vd[q] = valid ? v * st[q].dt : 0.0;                              // v*dt(i), rounded once (:64)
   }
-  if (!__all(fin)) {  // outside mcmcstat's finite parameter box: reported as NaN
+  if (!fin || nonfinite != 0) {  // outside mcmcstat's finite parameter box: reported as NaN
     write_nan<MODE>(lane, N, b, out0, out1, ld_out);
     return;
   }
@@ -279,16 +295,16 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
 #else
     const double excl = wave_shr1(wave_incl_scan(s));
 #endif
-    bool amb = false;
+    uint64_t amb = 0;
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
       const double Sq = excl + loc[q];
       const double eps = Sq * 0x1p-42;  // >> the (g + 16) ulp bound between any two summation orders
       const double Kq = floor(Sq);
-      amb = amb | (Sq - eps < Kq) | (Sq + eps >= Kq + 1.0);  // an integer within eps of Sq
+      amb |= wave_ballot(Sq - eps < Kq) | wave_ballot(Sq + eps >= Kq + 1.0);  // an integer within eps of Sq
       K[q] = Kq;
     }
-    if ((kp.force_exact & 1) || __any(amb)) {
+    if ((kp.force_exact & 1) || amb != 0) {
       // Exact path: the reference's serial loop, counter = counter + R(i)*dt(i).
 #pragma unroll
       for (int q = 0; q < RPL; ++q) simM[RPL * lane + q] = prod[q];
@@ -304,7 +320,7 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {
         const int g = RPL * lane + q;
-        K[q] = g < nsteps ? simP[g] : 0.0;
+        K[q] = simP[min(g, nsteps - 1)];  // constant past the last step, as the scan gives
       }
       wave_sync();
     }
@@ -343,40 +359,40 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
     if (fast) {
 #endif
       // ---- distance regions and their exactness proof
-      // |p(r, r-m) - P_m| <= m*v*delta + (m+3)*u*m*v*(d+delta) <= eps (taken at m = nsteps), doubled
-      const double mx = (double)nsteps;
-      const double eps = 2.0 * (mx * v * cm.delta + (mx + 4.0) * kUnitRoundoff * mx * v * (cm.d + cm.delta));
-      bool amb = false;
+      // |p(r, r-m) - P_m| <= v * (m*delta + (m+4)*u*m*(d+delta)) for every m <= nsteps; eps is
+      // twice that at m = nsteps, precomputed per cell up to the factor v (CellMeta::eps_v)
+      const double eps = v * cm.eps_v;
+      uint64_t amb = 0;
       int n_lt_L = 0;
-      int nM_le_a[NSEG], nM_lt_e[NSEG], nM_le_e[NSEG], nP_le_a[NSEG], nP_lt_e[NSEG], nP_le_e[NSEG];
+      // No P_m equals a threshold unless it is within eps > 0 of it (then the wave goes exact),
+      // so on the fast path #(P_m <= x) == #(P_m < x) and one count per threshold suffices.
+      int nM_a[NSEG], nM_e[NSEG], nP_a[NSEG], nP_e[NSEG];
 #pragma unroll
-      for (int k = 0; k < NSEG; ++k) nM_le_a[k] = nM_lt_e[k] = nM_le_e[k] = nP_le_a[k] = nP_lt_e[k] = nP_le_e[k] = 0;
+      for (int k = 0; k < NSEG; ++k) nM_a[k] = nM_e[k] = nP_a[k] = nP_e[k] = 0;
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {
         const int g = RPL * lane + q;
-        const bool valid = g < nsteps;
+        const uint64_t vmask = step_lanes<RPL>(nsteps, q);  // AND-ed on the scalar unit, not per vote
         const double md = (double)(g + 1);
         const double Pm = md * vd0;
         bool near = fabs(Pm - L) <= eps;
-        n_lt_L += count_true(valid & (Pm < L));
+        n_lt_L += __popcll(vmask & wave_ballot(Pm < L));
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) {
           near = near | (fabs(Pm - sm[k].a) <= eps) | (fabs(Pm - sm[k].e) <= eps) | (fabs(Pm - sp[k].a) <= eps) |
                  (fabs(Pm - sp[k].e) <= eps);
-          nM_le_a[k] += count_true(valid & (Pm <= sm[k].a));
-          nM_lt_e[k] += count_true(valid & (Pm < sm[k].e));
-          nM_le_e[k] += count_true(valid & (Pm <= sm[k].e));
-          nP_le_a[k] += count_true(valid & (Pm <= sp[k].a));
-          nP_lt_e[k] += count_true(valid & (Pm < sp[k].e));
-          nP_le_e[k] += count_true(valid & (Pm <= sp[k].e));
+          nM_a[k] += __popcll(vmask & wave_ballot(Pm < sm[k].a));
+          nM_e[k] += __popcll(vmask & wave_ballot(Pm < sm[k].e));
+          nP_a[k] += __popcll(vmask & wave_ballot(Pm < sp[k].a));
+          nP_e[k] += __popcll(vmask & wave_ballot(Pm < sp[k].e));
         }
-        amb = amb | (valid & near);
+        amb |= vmask & wave_ballot(near);
       }
-      fast = !__any(amb);
+      fast = amb == 0;
 #pragma unroll
       for (int k = 0; k < NSEG; ++k) {
-        rgM[k] = Regions{nM_le_a[k] + 1, nM_lt_e[k], nM_le_e[k] + 1, n_lt_L};
-        rgP[k] = Regions{nP_le_a[k] + 1, nP_lt_e[k], nP_le_e[k] + 1, n_lt_L};
+        rgM[k] = Regions{nM_a[k] + 1, nM_e[k], nM_e[k] + 1, n_lt_L};
+        rgP[k] = Regions{nP_a[k] + 1, nP_e[k], nP_e[k] + 1, n_lt_L};
       }
     }
     if (fast) {
@@ -387,8 +403,8 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
           const int g = RPL * lane + q;
-          const double cg = g < nsteps ? K[q] - (q == 0 ? kprev : K[q - 1]) : 0.0;
-          js = js + (double)g * cg;
+          const double cg = K[q] - (q == 0 ? kprev : K[q - 1]);  // 0 past the last step (K constant)
+          js = fma((double)g, cg, js);                           // integers < 2^53: exact
           jloc[q] = js;
         }
       }
@@ -417,7 +433,7 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
       }
     } else {
       // ---- exact systolic sweep: at iteration s slot g holds cohort g-s+1 with its forward position
-      double cc[RPL], p[RPL];
+      double cc[RPL], p[RPL], vd[RPL];
       {
         const double kprev = wave_shr1(K[RPL - 1]);
 #pragma unroll
@@ -426,6 +442,7 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
           const double km1 = q == 0 ? kprev : K[q - 1];
           cc[q] = g < nsteps ? K[q] - km1 : 0.0;
           p[q] = 0.0;
+          vd[q] = g < nsteps ? v * st[q].dt : 0.0;  // v*dt(i), rounded once (:64)
         }
       }
       for (int s = 1; s <= nsteps; ++s) {
@@ -440,7 +457,7 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
           p[0] = pin;
           cc[0] = cin;
         }
-        bool alive = false;
+        uint64_t alive = 0;
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
           p[q] = p[q] + vd[q];  // x(i+1,k) = x(i,k) + v*dt(i)
@@ -449,9 +466,9 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
             accM[k][q] = fma(cc[q], occupancy(p[q], sm[k], L), accM[k][q]);
             accP[k][q] = fma(cc[q], occupancy(p[q], sp[k], L), accP[k][q]);
           }
-          alive = alive | ((cc[q] > 0.0) & (p[q] < pstop) & (RPL * lane + q < nsteps));
+          alive |= step_lanes<RPL>(nsteps, q) & wave_ballot(cc[q] > 0.0) & wave_ballot(p[q] < pstop);
         }
-        if (!__any(alive)) break;
+        if (alive == 0) break;
       }
     }
   }
@@ -509,25 +526,23 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
   for (int kk = 0; kk < NPT; ++kk) {
     if (kk == RPL && N <= 64 * RPL) break;  // uniform: only N = 64*RPL + 1 has a tail point
     const int j = lane + 64 * kk;
-    if (j < N) {
-      const int k = (int)pt[kk].k;
-      double m = NAN, pp = NAN;
-      if (k >= 0) {
-        const double w = pt[kk].w;
-        m = fma(w, simM[k + 1] - simM[k], simM[k]);
-        pp = fma(w, simP[k + 1] - simP[k], simP[k]);
-      }
-      if (MODE == MODE_FWD_INTERP) {
+    // interp1: NaN outside the grid comes in through w = NaN (PointRec)
+    const int k = pt[kk].k;
+    const double w = pt[kk].w;
+    const double m = fma(w, simM[k + 1] - simM[k], simM[k]);
+    const double pp = fma(w, simP[k + 1] - simP[k], simP[k]);
+    if (MODE == MODE_FWD_INTERP) {
+      if (j < N) {
         out0[b * ld_out + j] = m;
         out1[b * ld_out + j] = pp;
-      } else {
-        double r1 = pt[kk].y1 - m;
-        r1 = r1 * r1;
-        double r2 = pt[kk].y2 - pp;
-        r2 = r2 * r2;
-        if (r1 == r1) ss += r1;  // nansum drops NaN data and NaN simulation alike
-        if (r2 == r2) ss += r2;
       }
+    } else {
+      // nansum drops NaN data, NaN simulation and the all-NaN padding points (j >= N) alike:
+      // fma(r, r, ss) >= ss unless it is NaN, and max() returns the non-NaN operand.
+      const double r1 = pt[kk].y1 - m;
+      ss = fmax(fma(r1, r1, ss), ss);
+      const double r2 = pt[kk].y2 - pp;
+      ss = fmax(fma(r2, r2, ss), ss);
     }
   }
   if (MODE == MODE_SS) {
