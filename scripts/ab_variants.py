@@ -24,6 +24,7 @@ VARIANTS = {
     "w6_noxcd": ["TCI_WAVES_PER_EU=6", "TCI_XCD_REMAP=0"],
     "w8_latepts": ["TCI_WAVES_PER_EU=8", "TCI_EARLY_POINTS=0"],
     "loopramp": ["TCI_RAMP_PREFIX=0"],
+    "abl_loads": ["TCI_ABLATE=16"],
 }
 
 

@@ -59,8 +59,8 @@
 #define TCI_EARLY_POINTS 1   // issue the acquisition-point loads with the first round trip
 #endif
 #ifndef TCI_ABLATE
-#define TCI_ABLATE 0         // diagnostics only (wrong results): bit0 rows, bit1 bounds, bit2 interp, bit3 scan
-#endif
+#define TCI_ABLATE 0         // diagnostics only (wrong results): bit0 rows, bit1 bounds, bit2 interp, bit3 scan,
+#endif                       // bit4 loads only
 #ifndef TCI_WAVES_PER_EU
 #define TCI_WAVES_PER_EU 6   // register budget for 6 waves/SIMD (A/B: 50 us vs 58 us at the
 #endif                       // compiler's default 5 waves; 7-8 waves no faster)
@@ -152,28 +152,29 @@ struct Regions {
 //   K_i = sum_{i' <= i} c_i'        (= floor(counter_i): polymerases loaded through step i)
 //   J_i = sum_{i' <= i} i' * c_i'
 // Both are integers < 2^53, exact in any summation order. KJ points at i = 0 of a table whose
-// SLOTS entries below i = 0 are zeros, so every index r - m - 1 >= -SLOTS needs no clamp.
+// SLOTS+RPL entries below i = 0 are zeros, so every index r - m - 1 >= -SLOTS needs no clamp.
 __device__ __forceinline__ double2 kj_at(const double2* KJ, int i) { return KJ[i]; }
 
 // Row sum of one segment of one dye on the fast path (see the header), O(1) per row:
 //   full  (e < P_m < L, m in [f_lo, f_hi]):  phi * (K[r - f_lo] - K[r - f_hi - 1])
 //   ramp  (a < P_m < e, m in [r_lo, r_hi]):  sum_m c_{r-m} * (m*vd0 - a) * k
-//        = k * (vd0 * sum_m m*c_{r-m}  -  a * sum_m c_{r-m}),   sum_m m*c_{r-m} = r*C - (J_hi - J_lo)
-__device__ __forceinline__ double row_sum(const double2* KJ, int r, const Regions& rg, const SegParams& s,
-                                          double vd0) {
+//        = (k*vd0) * sum_m m*c_{r-m}  -  (k*a) * sum_m c_{r-m},   sum_m m*c_{r-m} = r*C - (J_hi - J_lo)
+// kvd = k*vd0 and ka = k*a are wave constants; C, J differences and r*C - dJ are exact integers.
+__device__ __forceinline__ double row_sum(const double2* KJ, int r, double rd, const Regions& rg,
+                                          const SegParams& s, double kvd, double ka) {
   double acc = 0.0;
   if (rg.f_lo <= rg.f_hi) acc = s.phi * (kj_at(KJ, r - rg.f_lo).x - kj_at(KJ, r - rg.f_hi - 1).x);
   if (rg.r_lo <= rg.r_hi) {
 #if TCI_RAMP_PREFIX
     const double2 hi = kj_at(KJ, r - rg.r_lo), lo = kj_at(KJ, r - rg.r_hi - 1);
     const double C = hi.x - lo.x;
-    const double Mc = (double)r * C - (hi.y - lo.y);  // sum of m * c_{r-m}, exact
-    acc += s.k * (vd0 * Mc - s.a * C);
+    const double Mc = fma(rd, C, -(hi.y - lo.y));  // sum of m * c_{r-m}, exact
+    acc = fma(kvd, Mc, fma(-ka, C, acc));
 #else
     double kA = kj_at(KJ, r - rg.r_lo).x;
     for (int m = rg.r_lo; m <= rg.r_hi; ++m) {
       const double kB = kj_at(KJ, r - m - 1).x;
-      acc = fma(kA - kB, ((double)m * vd0 - s.a) * s.k, acc);
+      acc = fma(kA - kB, fma((double)m, kvd, -ka), acc);
       kA = kB;
     }
 #endif
@@ -197,9 +198,11 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
                                                          double* __restrict__ out0, double* __restrict__ out1,
                                                          int64_t ld_out) {
   constexpr int SLOTS = 64 * RPL;      // rows 1..SLOTS (row 0 never holds a polymerase)
-  constexpr int SIMP = SLOTS + 2;      // offset of the PP7 row array
+  // Simulated rows j = 0..SLOTS of each dye: simM[j] = lds[1 + j], simP[j] = lds[SLOTS + 3 + j],
+  // so a lane's first row RPL*lane + 1 starts 16-B aligned (paired 16-B row stores).
+  constexpr int SIMM = 1, SIMP = SLOTS + 3;
   constexpr int NPT = RPL + 1;         // acquisition points per lane (N <= 64*RPL + 1)
-  constexpr int WAVE_DOUBLES = 4 * SLOTS + 4;  // {K,J} table (2*SLOTS+1 entries) / the two sim rows
+  constexpr int WAVE_DOUBLES = 4 * SLOTS + 4 * RPL;  // {K,J} table (2*SLOTS+RPL entries) / the two sim rows
   __shared__ __attribute__((aligned(16))) double s_lds[kWavesPerBlock][WAVE_DOUBLES];
 
   const int lane = threadIdx.x & 63;
@@ -216,8 +219,9 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
   const int64_t b = (int64_t)vb * kWavesPerBlock + wid;
   if (b >= B) return;
   double* lds = s_lds[wid];
-  double* simM = lds;
+  double* simM = lds + SIMM;
   double* simP = lds + SIMP;
+  static_assert(SIMP + SLOTS + 1 <= WAVE_DOUBLES, "sim rows exceed the wave's LDS");
 
   // ---- every load of the evaluation is issued here, in one round trip
   const int c = __builtin_amdgcn_readfirstlane(cell_id[b]);
@@ -260,6 +264,18 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
     return;
   }
   const int nsteps = N - 1;  // loading steps = rows that can hold polymerases
+#if TCI_ABLATE & 16
+  if (MODE == MODE_SS) {  // memory floor: every load, no compute
+    double x = v + tau + ton + b1 + b2 + A + R + cm.d;
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) x += dr[q] + st[q].dt + st[q].t;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) x += pt[k].w + pt[k].y1 + pt[k].y2 + (double)pt[k].k;
+    x = lane63(wave_incl_scan(x));
+    if (lane == 0) out0[b] = x;
+    return;
+  }
+#endif
 
   // ---- per-step setup: R_full = R + dR (SumofSquares...m:45); R<0 -> 0 (ConstantElongationSim.m:36)
   double prod[RPL];
@@ -409,25 +425,35 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
         }
       }
       const double jexcl = wave_shr1(wave_incl_scan(js));
-      double2* KJ = reinterpret_cast<double2*>(lds) + SLOTS + 1;  // KJ[i], i in [-SLOTS-1, SLOTS)
+      // KJ[i], i in [-SLOTS-RPL, SLOTS): the SLOTS+RPL entries below i = 0 are zeros
+      double2* KJ = reinterpret_cast<double2*>(lds) + SLOTS + RPL;
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {
         KJ[RPL * lane + q] = make_double2(K[q], jexcl + jloc[q]);
-        KJ[RPL * lane + q - SLOTS - 1] = make_double2(0.0, 0.0);
+        KJ[RPL * lane + q - SLOTS - RPL] = make_double2(0.0, 0.0);
+        if (lane == 0) KJ[q - RPL] = make_double2(0.0, 0.0);
       }
-      if (lane == 0) KJ[-1] = make_double2(0.0, 0.0);
       wave_sync();
+      double kvdM[NSEG], kaM[NSEG], kvdP[NSEG], kaP[NSEG];
+#pragma unroll
+      for (int k = 0; k < NSEG; ++k) {
+        kvdM[k] = sm[k].k * vd0;
+        kaM[k] = sm[k].k * sm[k].a;
+        kvdP[k] = sp[k].k * vd0;
+        kaP[k] = sp[k].k * sp[k].a;
+      }
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {
         const int r = RPL * lane + q + 1;
+        const double rd = (double)r;
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) {
 #if TCI_ABLATE & 1
           accM[k][q] = KJ[r].x + (double)rgM[k].f_lo;
           accP[k][q] = KJ[r].y + (double)rgP[k].f_hi;
 #else
-          accM[k][q] = row_sum(KJ, r, rgM[k], sm[k], vd0);
-          accP[k][q] = row_sum(KJ, r, rgP[k], sp[k], vd0);
+          accM[k][q] = row_sum(KJ, r, rd, rgM[k], sm[k], kvdM[k], kaM[k]);
+          accP[k][q] = row_sum(KJ, r, rd, rgP[k], sp[k], kvdP[k], kaP[k]);
 #endif
         }
       }
@@ -475,19 +501,28 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
   wave_sync();  // every {K,J}-table read is done before the rows overwrite the LDS
 
   // ---- basal floor inside the segment loop (GetFluorFromPolPos.m:54-57,66-69), x A (SumofSquares...m:51)
+  //      Rows past the last step are stored too (never read): stores stay whole 16-B pairs.
+  double rowM[RPL], rowP[RPL];
 #pragma unroll
   for (int q = 0; q < RPL; ++q) {
-    const int g = RPL * lane + q;
-    if (g < nsteps) {
-      // MS2(MS2 < basal) = basal == max(MS2, basal): the sums are finite and >= 0 here
-      double m = 0.0, pp = 0.0;
+    // MS2(MS2 < basal) = basal == max(MS2, basal): the sums are finite and >= 0 here
+    double m = fmax(accM[0][q], b1), pp = fmax(accP[0][q], b2);
 #pragma unroll
-      for (int k = 0; k < NSEG; ++k) {
-        m = fmax(m + accM[k][q], b1);
-        pp = fmax(pp + accP[k][q], b2);
-      }
-      simM[g + 1] = A * m;
-      simP[g + 1] = pp;
+    for (int k = 1; k < NSEG; ++k) {
+      m = fmax(m + accM[k][q], b1);
+      pp = fmax(pp + accP[k][q], b2);
+    }
+    rowM[q] = A * m;
+    rowP[q] = pp;
+  }
+  if (RPL == 1) {
+    simM[lane + 1] = rowM[0];
+    simP[lane + 1] = rowP[0];
+  } else {
+#pragma unroll
+    for (int q = 0; q < RPL; q += 2) {
+      *reinterpret_cast<double2*>(simM + RPL * lane + q + 1) = make_double2(rowM[q], rowM[q + 1]);
+      *reinterpret_cast<double2*>(simP + RPL * lane + q + 1) = make_double2(rowP[q], rowP[q + 1]);
     }
   }
   if (lane == 0) {  // first row of the reference: no polymerase yet
