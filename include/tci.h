@@ -147,7 +147,19 @@ typedef struct {
   int64_t stats_from;   /* first chain row (1-based) of the posterior summaries (n_burn, :276) */
   int64_t thin;         /* keep every thin-th chain row in outputs.chain (0 = keep none) */
   uint64_t seed;
+  int32_t engine;       /* TCI_DRAM_AUTO / TCI_DRAM_FUSED / TCI_DRAM_BATCHED (below) */
+  int32_t reserved;
 } tci_dram_options;
+
+/* DRAM engines; both give identical chains for the same seed.
+ *   FUSED:   one workgroup per chain runs a chunk of steps (up to the next adaptation) inside one
+ *            kernel, with its ssfun evaluations in the loop: latency-bound runs (few chains).
+ *   BATCHED: one launch per stage, every chain's ssfun in the batched likelihood kernel, replayed
+ *            as a hipGraph per adaptation window: many chains, or cells too long for FUSED.
+ *   AUTO:    FUSED when every chain fits it (npar <= 520) and there are at most 8 chains per CU. */
+#define TCI_DRAM_AUTO 0
+#define TCI_DRAM_FUSED 1
+#define TCI_DRAM_BATCHED 2
 
 /* Host buffers filled by tci_dram_run (any may be NULL). Per-chain vectors have stride ld. */
 typedef struct {
@@ -160,6 +172,8 @@ typedef struct {
   int64_t* n_evals;     /* ssfun calls: the initial one + every in-bounds proposal */
   double* chain;        /* [ceil(n_steps/thin)][n_chains][ld] thinned rows (rows 1, 1+thin, ...) */
   double* s2chain;      /* [ceil(n_steps/thin)][n_chains] */
+  double* qcov_R;       /* [n_chains][ld][ld] final proposal factor R (upper): qcov = R'R (mcmcstat results.qcov) */
+  double* qcov_iR;      /* [n_chains][ld][ld] its inverse (upper), used by the delayed-rejection ratio */
   double elapsed_ms;    /* device time of the step loop (HIP events) */
 } tci_dram_outputs;
 

@@ -9,14 +9,15 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from transcriptioncycleinference_amd import Likelihood, testdata  # noqa: E402
-from transcriptioncycleinference_amd.mcmc import fit  # noqa: E402
+from transcriptioncycleinference_amd.mcmc import DramOptions, fit  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
-lk = Likelihood(testdata())
+engine = sys.argv[2] if len(sys.argv) > 2 else "auto"
+lk = Likelihood(testdata(), lib_path=os.environ.get("TCI_LIB"))  # TCI_LIB: an A/B build variant
 t0 = time.perf_counter()
-fr = fit(lk, n_steps=steps, n_burn=steps // 2, seed=1)
+fr = fit(lk, n_steps=steps, n_burn=steps // 2, seed=1, opts=DramOptions(engine=engine))
 wall = time.perf_counter() - t0
-print(json.dumps({"n_steps": steps, "chains": len(fr.MCMCresults), "device_ms": fr.elapsed_ms, "wall_s": wall,
+print(json.dumps({"engine": engine, "n_steps": steps, "chains": len(fr.MCMCresults), "device_ms": fr.elapsed_ms, "wall_s": wall,
                   "us_per_step": fr.elapsed_ms * 1e3 / (steps - 1), "ssfun_evals": fr.n_evals,
                   "evals_per_s": fr.n_evals / (fr.elapsed_ms * 1e-3),
                   "accept_rate_median": float(np.median(fr.accept_rate))}))

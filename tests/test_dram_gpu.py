@@ -240,3 +240,48 @@ def test_fit_skips_cells_without_previous_v(lk):
     fr = fit(lk, n_steps=50, n_burn=10, cells=[0, 1, 2, 3], v0=[1.5, None, float("nan"), 2.0])
     assert [r["cell_index"] for r in fr.MCMCresults] == [1, 4]
     assert all(abs(r["mean_v"] - v) <= 1e-5 for r, v in zip(fr.MCMCresults, [1.5, 2.0]))
+
+
+@pytest.mark.parametrize("ntry", [2, 1])
+def test_fused_and_batched_engines_give_identical_chains(lk, ntry):
+    """The fused engine (one workgroup per chain, ssfun inside the step loop) and the batched
+    engine (one launch per stage, graph-replayed) share RNG keys, reductions and operation order:
+    every output must be bitwise equal, through burn-in scaling, covariance adaptation and a
+    tail shorter than adaptint."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions
+
+    ids = list(range(0, 299, 5))
+    o = DramOptions(n_steps=650, burnintime=300, adaptint=100, stats_from=200, thin=7, seed=11, ntry=ntry)
+    o.engine = "fused"
+    a, _ = run(lk, ids, o)
+    o.engine = "batched"
+    b, _ = run(lk, ids, o)
+    for f in ("chain", "s2chain", "mean", "std", "final_theta", "sigma_mean", "sigma_std", "accept_rate", "n_evals"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    assert np.median(a.accept_rate) > 0.01
+
+
+@pytest.mark.parametrize("engine", ["fused", "batched"])
+def test_adapted_proposal_is_the_scaled_chain_covariance(lk, engine):
+    """mcmcstat's adaptation: after the last adaptation row n (n >= burnintime), the proposal
+    factor satisfies R'R = (2.4/sqrt(P))^2 (cov(chain rows 1..n) + qcovadj I) with the sample
+    covariance of every row so far (covupd's recurrence), and iR = R^-1."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions
+
+    ids = list(range(0, 299, 37))
+    o = DramOptions(n_steps=700, burnintime=300, adaptint=100, stats_from=1, thin=1, seed=21, engine=engine)
+    x0, lo, hi, mu, sg, J0 = setup_rows(lk.cells, ids, 0)
+    from transcriptioncycleinference_amd.mcmc import dram_run
+
+    res = dram_run(lk, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, want_qcov=True)
+    n = lk.cells.lengths[ids]
+    for k in range(len(ids)):
+        P = 7 + int(n[k])
+        X = res.chain[:700, k, :P]
+        C = np.cov(X.T, ddof=1) + 1e-5 * np.eye(P)
+        R = res.qcov_R[k, :P, :P]
+        assert np.all(np.tril(R, -1) == 0)
+        Q = R.T @ R
+        want = (2.4 ** 2 / P) * C
+        np.testing.assert_allclose(Q, want, rtol=1e-7, atol=1e-9 * np.abs(want).max())
+        np.testing.assert_allclose(R @ res.qcov_iR[k, :P, :P], np.eye(P), atol=1e-8)

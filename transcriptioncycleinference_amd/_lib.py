@@ -59,13 +59,13 @@ class tci_dram_options(C.Structure):
     _fields_ = [("n_steps", C.c_int64), ("burnintime", C.c_int64), ("adaptint", C.c_int64), ("ntry", C.c_int32),
                 ("updatesigma", C.c_int32), ("drscale", C.c_double), ("adascale", C.c_double),
                 ("qcovadj", C.c_double), ("burnin_scale", C.c_double), ("stats_from", C.c_int64),
-                ("thin", C.c_int64), ("seed", C.c_uint64)]
+                ("thin", C.c_int64), ("seed", C.c_uint64), ("engine", C.c_int32), ("reserved", C.c_int32)]
 
 
 class tci_dram_outputs(C.Structure):
     _fields_ = [("mean", _dp), ("std", _dp), ("final_theta", _dp), ("sigma_mean", _dp), ("sigma_std", _dp),
-                ("accept_rate", _dp), ("n_evals", _i64p), ("chain", _dp), ("s2chain", _dp),
-                ("elapsed_ms", C.c_double)]
+                ("accept_rate", _dp), ("n_evals", _i64p), ("chain", _dp), ("s2chain", _dp), ("qcov_R", _dp),
+                ("qcov_iR", _dp), ("elapsed_ms", C.c_double)]
 
 
 # (name, restype, argtypes) for every symbol declared in include/tci.h

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cmath>
 #include <cstring>
 #include <new>
@@ -503,6 +504,8 @@ int tci_dram_defaults(tci_dram_options* o) {
   o->stats_from = 10000;  // chain(n_burn:end, :) (:276)
   o->thin = 0;
   o->seed = 20201028;
+  o->engine = TCI_DRAM_AUTO;
+  o->reserved = 0;
   return TCI_OK;
 }
 
@@ -514,8 +517,10 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   if (!opt || !out || n_chains <= 0 || !cell_id || !theta0 || !lower || !upper || !prior_mu || !prior_sig ||
       !qcov_diag || !sigma2_0)
     return fail(ctx, TCI_EINVAL, "tci_dram_run: null argument or no chains");
-  if (opt->n_steps < 1 || opt->ntry < 1 || opt->ntry > 2 || opt->adaptint < 0 || !(opt->drscale > 0))
-    return fail(ctx, TCI_EINVAL, "tci_dram_run: bad options (n_steps >= 1, ntry in {1,2}, adaptint >= 0)");
+  if (opt->n_steps < 1 || opt->ntry < 1 || opt->ntry > 2 || opt->adaptint < 0 || !(opt->drscale > 0) ||
+      opt->engine < TCI_DRAM_AUTO || opt->engine > TCI_DRAM_BATCHED)
+    return fail(ctx, TCI_EINVAL,
+                "tci_dram_run: bad options (n_steps >= 1, ntry in {1,2}, adaptint >= 0, engine in {0,1,2})");
   int rc = check_rows(ctx, ld, cell_id, n_chains);
   if (rc != TCI_OK) return rc;
   if (ld > TCI_MAX_POINTS + 7) return fail(ctx, TCI_ERANGE, "tci_dram_run: ld too large");
@@ -594,6 +599,10 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(sq_mean, double, n);
   TCI_ALLOC(sq_m2, double, n);
   TCI_ALLOC(step, int64_t, 1);
+#ifdef TCI_CHAIN_PROFILE
+  TCI_ALLOC(prof, int64_t, 8);
+  TCI_HIP(ctx, hipMemsetAsync(st.prof, 0, 8 * sizeof(int64_t), ctx->stream));
+#endif
   if (n_keep > 0 && (out->chain || out->s2chain)) {
     TCI_ALLOC(chain_out, double, (size_t)n_keep * n * L);
     TCI_ALLOC(s2_out, double, (size_t)n_keep * n);
@@ -636,19 +645,37 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_HIP(ctx, hipEventCreate(&ev0));
   TCI_HIP(ctx, hipEventCreate(&ev1));
   TCI_HIP(ctx, hipEventRecord(ev0, s));
-  // The step loop. Steps 2 .. n_steps; adaptation after steps that are multiples of adaptint.
-  // Blocks of adaptint steps (aligned so that each ends on an adaptation step) are captured once
-  // as a hipGraph and replayed; the head (steps 2..adaptint) and the tail run as plain launches.
   int64_t p_max = 0;
   for (size_t c = 0; c < n; ++c) p_max = std::max<int64_t>(p_max, npar[c]);
   p.lds_matrix = p_max * p_max * (int64_t)sizeof(double) <= 150 * 1024 ? p_max * p_max * (int64_t)sizeof(double) : 0;
+  p.pmax = p_max;
   const int64_t ai = opt->adaptint;
+  int n_cu = 0;
+  TCI_HIP(ctx, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  const bool fused_fits = tci::dram_chain_lds_bytes(ld, ctx->rpl) <= 64 * 1024;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  bool fused = opt->engine == TCI_DRAM_FUSED;
+  if (opt->engine == TCI_DRAM_AUTO) fused = fused_fits && n_chains <= 8 * (int64_t)std::max(n_cu, 1);
+  if (fused && !fused_fits) return fail(ctx, TCI_ERANGE, "tci_dram_run: rows too long for the fused engine");
+  if (fused) {
+    // Chunks of chain rows up to the next adaptation row; k_chain leaves *st.step at the chunk end.
+    const int64_t G = ai > 0 ? ai : 1000;
+    for (int64_t next = 2; next <= opt->n_steps && rc == TCI_OK;) {
+      const int64_t end = std::min<int64_t>(opt->n_steps, ((next + G - 1) / G) * G);
+      rc = tci::dram_launch_chain(st, p, ctx->kp, ctx->rpl, next, end, s);
+      if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(st, p, s);
+      next = end + 1;
+    }
+    e = hipSuccess;
+  } else {
+  // The step loop. Steps 2 .. n_steps; adaptation after steps that are multiples of adaptint.
+  // Blocks of adaptint steps (aligned so that each ends on an adaptation step) are captured once
+  // as a hipGraph and replayed; the head (steps 2..adaptint) and the tail run as plain launches.
   int64_t next = 2;  // next step number to enqueue
   auto plain = [&](int64_t upto) {  // steps next .. upto
     for (; next <= upto && rc == TCI_OK; ++next) rc = enqueue_step(ctx, st, p, s, ai > 0 && next % ai == 0);
   };
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
   const int64_t G = ai > 0 ? ai : 50;
   if (ai > 0) plain(std::min<int64_t>(ai, opt->n_steps));  // head: up to the first adaptation step
   const int64_t blocks = (opt->n_steps - next + 1) / G;
@@ -670,11 +697,22 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
     next += blocks * G;
   }
   if (e == hipSuccess) plain(opt->n_steps);  // tail
+  }
   const hipError_t ge = e;
   TCI_HIP(ctx, hipEventRecord(ev1, s));
   TCI_HIP(ctx, hipStreamSynchronize(s));
   if (exec) (void)hipGraphExecDestroy(exec);
   if (graph) (void)hipGraphDestroy(graph);
+#ifdef TCI_CHAIN_PROFILE
+  {
+    int64_t ph[8];
+    TCI_HIP(ctx, hipMemcpy(ph, st.prof, sizeof(ph), hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "{\"k_chain_phase_cycles_per_chain_step\": [");
+    for (int k = 0; k < 8; ++k)
+      std::fprintf(stderr, "%s%.1f", k ? ", " : "", (double)ph[k] / (double)n / (double)std::max<int64_t>(opt->n_steps - 1, 1));
+    std::fprintf(stderr, "]}\n");
+  }
+#endif
   if (ge != hipSuccess) return hip_fail(ctx, ge, "DRAM step replay");
   if (rc != TCI_OK) return fail(ctx, rc, "DRAM step launch");
   float ms = 0.f;
@@ -708,6 +746,8 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   if (out->final_theta) TCI_HIP(ctx, hipMemcpy(out->final_theta, st.theta, n * L * sizeof(double), hipMemcpyDeviceToHost));
   if (st.chain_out && out->chain)
     TCI_HIP(ctx, hipMemcpy(out->chain, st.chain_out, (size_t)n_keep * n * L * sizeof(double), hipMemcpyDeviceToHost));
+  if (out->qcov_R) TCI_HIP(ctx, hipMemcpy(out->qcov_R, st.R, n * L2 * sizeof(double), hipMemcpyDeviceToHost));
+  if (out->qcov_iR) TCI_HIP(ctx, hipMemcpy(out->qcov_iR, st.iR, n * L2 * sizeof(double), hipMemcpyDeviceToHost));
   if (st.s2_out && out->s2chain)
     TCI_HIP(ctx, hipMemcpy(out->s2chain, st.s2_out, (size_t)n_keep * n * sizeof(double), hipMemcpyDeviceToHost));
   return TCI_OK;

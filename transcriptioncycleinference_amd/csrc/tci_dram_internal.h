@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "tci.h"
+#include "tci_internal.h"
 
 namespace tci {
 
@@ -50,6 +51,7 @@ struct DramState {
   double* s2_out;          // optional thinned s2 rows
   double* work;            // Cholesky workspace (n_chains x ld x ld)
   int64_t* step;           // current chain row (1-based), advanced on device after each step
+  int64_t* prof;           // TCI_CHAIN_PROFILE builds only: cycles per k_chain phase, summed over chains
 };
 
 struct DramParams {
@@ -66,6 +68,7 @@ struct DramParams {
   int64_t thin;
   int64_t n_keep;
   int64_t lds_matrix;  // bytes of dynamic LDS for the adaptation matrix (0 = work in global memory)
+  int64_t pmax;        // max parameter count over the chains (picks the adaptation kernel)
 };
 
 int dram_launch_init(const DramState& st, const double* qcov_diag, const double* sigma2_0, void* stream);
@@ -75,5 +78,9 @@ int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream);
 int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream);  // no-op unless step % adaptint == 0
 int dram_launch_step_incr(const DramState& st, void* stream);
 int dram_launch_init_stats(const DramState& st, const DramParams& p, void* stream);
+// Fused engine: chain rows s_begin..s_end (each chain's ssfun inside the kernel); leaves *st.step = s_end.
+int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,
+                      int64_t s_end, void* stream);
+int64_t dram_chain_lds_bytes(int64_t ld, int rpl);  // LDS per workgroup of the fused engine
 
 }  // namespace tci

@@ -1,66 +1,11 @@
-// tci_kernels.hip -- batched FP64 likelihood kernel for gfx950 (CDNA4).
-//
-// One wavefront (64 lanes) evaluates one ssfun(theta, cell):
-//   SumofSquaresFunction_TranscriptionCycleMCMC.m:1-64
-//     -> ConstantElongationSim.m:1-67 -> GetFluorFromPolPos.m:1-71
-// without ever materialising the reference's time x polymerase matrix.
-//
-// Cohort form. Every polymerase loaded at grid step i (ConstantElongationSim.m:60-64) has the
-// same position at every later row r:  p(r,i) = (..((v*dt_i) + v*dt_{i+1}) + ..) + v*dt_{r-1},
-// accumulated FORWARD exactly as x(i+1,k) = x(i,k) + v*dt(i) does. The
-// c_i = floor(counter_i) - floor(counter_{i-1}) polymerases of step i form one cohort, so a
-// row's stem-loop sum over polymerases is  sum_i c_i * f(p(r,i))  (GetFluorFromPolPos.m:47-66).
-//
-// Lane layout. Lane l owns RPL consecutive rows (slots g = RPL*l + q hold row g+1). Cohort
-// values travel between slots by register rename inside a lane and one DPP wave_shr:1 across
-// lanes, so row accumulators never leave registers.
-//
-// Loading counter. counter = counter + R(i)*dt(i) (multiply, then add; no FMA) feeds floor().
-// A wave-parallel prefix sum gives every step's counter within a proven bound (<= ~530 ulp of
-// the sum); floor() is taken from it unless a step lands within 2^-42 (relative) of an integer,
-// in which case the wave runs the reference's serial loop (LDS, lane 0). Bit-identical to the
-// serial MATLAB loop either way.
-//
-// Positions, fast path (uniform grid). The SS grid is t(1):d:t(end), so every step's v*dt is
-// v*d up to a few ulps (delta = max |dt_j - d| is precomputed per cell). A cohort's position
-// after m steps is then m*v*d within a proven bound eps_m, for EVERY cohort. If no
-// representative position P_m = m*(v*d) lies within eps_m of a decision threshold (loop
-// starts/ends, gene end L: the strict < / > of GetFluorFromPolPos.m:50-51,62-63), every
-// (row, cohort) pair at distance m takes the branch the reference takes, so the occupancy is a
-// function of the distance alone: 0 while P_m <= a, a ramp (P_m - a)*phi/(e - a) while
-// a < P_m < e, phi while e < P_m < L, 0 after. With K_i = floor(counter_i) the exact cumulative
-// number of polymerases loaded through step i, a row's sum over all polymerases is then
-//   phi * (K[r - f_lo] - K[r - f_hi - 1])  +  sum_{m in ramp} (K[r-m] - K[r-m-1]) * F(m)
-// -- O(1 + ramp length) per row instead of one term per polymerase (the reference) or per
-// cohort. The ramp values use P_m instead of each cohort's exact position: ulp-level only.
-//
-// Positions, exact path. Otherwise (an ambiguous distance, the raw non-uniform grid of the
-// plot/summary forward model, or the test hook) the wave runs the systolic sweep: each cohort
-// carries its exactly-accumulated forward position, one add per (row, cohort) pair in the
-// reference's order, and every branch is decided on bit-identical positions.
-//
-// This file is compiled with -ffp-contract=off (see build.py) so hipcc never fuses the
-// multiply-then-add statements that feed floor() and the strict comparisons. Continuous parts
-// (row sums, interp1, the residual sum) use explicit FMA and wave reductions; they differ from
-// MATLAB only at the ulp level.
-#include <hip/hip_runtime.h>
-#include <math.h>
-
-#include "tci_internal.h"
+// tci_kernels.hip -- batched FP64 likelihood kernel for gfx950 (CDNA4): one wavefront per
+// ssfun(theta, cell) evaluation (the algorithm and its exactness arguments: tci_eval.h).
+#include "tci_eval.h"
 
 // Build-time variants for A/B timing (scripts/ab_variants.py); the shipped defaults are below.
 #ifndef TCI_XCD_REMAP
 #define TCI_XCD_REMAP 0      // XCD-aware block -> row-range order (A/B: ~1% slower here; the
 #endif                       // 3.7 MB cell table fits every XCD's L2 anyway)
-#ifndef TCI_RAMP_PREFIX
-#define TCI_RAMP_PREFIX 1    // O(1) ramp via the J prefix table (else a loop over ramp distances)
-#endif
-#ifndef TCI_EARLY_POINTS
-#define TCI_EARLY_POINTS 1   // issue the acquisition-point loads with the first round trip
-#endif
-#ifndef TCI_ABLATE
-#define TCI_ABLATE 0         // diagnostics only (wrong results): bit0 rows, bit1 bounds, bit2 interp, bit3 scan,
-#endif                       // bit4 loads only
 #ifndef TCI_WAVES_PER_EU
 #define TCI_WAVES_PER_EU 6   // register budget for 6 waves/SIMD (A/B: 50 us vs 58 us at the
 #endif                       // compiler's default 5 waves; 7-8 waves no faster)
@@ -76,121 +21,6 @@ namespace {
 
 constexpr int kWavesPerBlock = 4;
 
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ double dpp_f64(double x) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, ROW_MASK, 0xF, true);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, ROW_MASK, 0xF, true);
-  return __hiloint2double(hi, lo);
-}
-
-// DPP wave_shr:1 (GFX9 family; dpp_ctrl 0x138): lane l receives lane l-1, lane 0 gets 0.
-__device__ __forceinline__ double wave_shr1(double x) { return dpp_f64<0x138, 0xF>(x); }
-
-// Inclusive wave64 prefix sum in registers (DPP row_shr 1/2/4/8 inside 16-lane rows, then
-// row_bcast:15 and row_bcast:31 across rows): no LDS round trips.
-__device__ __forceinline__ double wave_incl_scan(double x) {
-  x = x + dpp_f64<0x111, 0xF>(x);
-  x = x + dpp_f64<0x112, 0xF>(x);
-  x = x + dpp_f64<0x114, 0xF>(x);
-  x = x + dpp_f64<0x118, 0xF>(x);
-  x = x + dpp_f64<0x142, 0xA>(x);
-  x = x + dpp_f64<0x143, 0xC>(x);
-  return x;
-}
-
-__device__ __forceinline__ double lane63(double x) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(x), 63);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), 63);
-  return __hiloint2double(hi, lo);
-}
-
-// Order LDS traffic between lanes of ONE wavefront (a wave's LDS ops execute in order; this
-// only stops the compiler from moving accesses across the point).
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Wave votes straight on the compare mask (the int-predicate __ballot/__any/__all round-trip
-// every bool through a VGPR select and a compare: two extra VALU per vote).
-// Votes are OR-ed / AND-ed as 64-bit masks on the scalar unit; the ballot operand is kept a
-// single compare.
-__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-
-// Mask of the lanes l whose slot RPL*l + q is a loading step (g < nsteps), built on the scalar
-// unit: lanes 0 .. ceil((nsteps - q) / RPL) - 1.
-template <int RPL>
-__device__ __forceinline__ uint64_t step_lanes(int nsteps, int q) {
-  const int n = nsteps > q ? (nsteps - q + RPL - 1) / RPL : 0;
-  return n >= 64 ? ~0ull : (1ull << n) - 1;
-}
-
-// Exponent field of a double: all ones iff the value is +-Inf or NaN. The max over the
-// wave-uniform theta entries stays on the scalar unit (isfinite() would be a vector compare each).
-__device__ __forceinline__ unsigned exp_bits(double x) { return (unsigned)__double2hiint(x) & 0x7ff00000u; }
-
-// Stem-loop occupancy of one polymerase at position p (GetFluorFromPolPos.m:50-52):
-//   phi                 if e < p < L
-//   (p - a)*phi/(e-a)   if a < p < e      (slope precomputed: ulp-level difference only)
-//   0                   otherwise (strict inequalities: p == e gives 0).
-// p <= a makes (p-a)*k <= 0, so max(.,0) realises the p > a test exactly.
-__device__ __forceinline__ double occupancy(double p, const SegParams& s, double L) {
-  double fr = (p - s.a) * s.k;
-  fr = fr > 0.0 ? fr : 0.0;
-  const double full = (p > s.e && p < L) ? s.phi : 0.0;
-  return p < s.e ? fr : full;
-}
-
-// Distance-table regions of one segment of one dye: ramp m in [r_lo, r_hi] (a < P_m < e),
-// full m in [f_lo, f_hi] (e < P_m < L). Empty ranges have lo > hi.
-struct Regions {
-  int r_lo, r_hi, f_lo, f_hi;
-};
-
-// Exact prefix tables of the fast path, interleaved per cohort index i (LDS, 16 B per entry):
-//   K_i = sum_{i' <= i} c_i'        (= floor(counter_i): polymerases loaded through step i)
-//   J_i = sum_{i' <= i} i' * c_i'
-// Both are integers < 2^53, exact in any summation order. KJ points at i = 0 of a table whose
-// SLOTS+RPL entries below i = 0 are zeros, so every index r - m - 1 >= -SLOTS needs no clamp.
-__device__ __forceinline__ double2 kj_at(const double2* KJ, int i) { return KJ[i]; }
-
-// Row sum of one segment of one dye on the fast path (see the header), O(1) per row:
-//   full  (e < P_m < L, m in [f_lo, f_hi]):  phi * (K[r - f_lo] - K[r - f_hi - 1])
-//   ramp  (a < P_m < e, m in [r_lo, r_hi]):  sum_m c_{r-m} * (m*vd0 - a) * k
-//        = (k*vd0) * sum_m m*c_{r-m}  -  (k*a) * sum_m c_{r-m},   sum_m m*c_{r-m} = r*C - (J_hi - J_lo)
-// kvd = k*vd0 and ka = k*a are wave constants; C, J differences and r*C - dJ are exact integers.
-__device__ __forceinline__ double row_sum(const double2* KJ, int r, double rd, const Regions& rg,
-                                          const SegParams& s, double kvd, double ka) {
-  double acc = 0.0;
-  if (rg.f_lo <= rg.f_hi) acc = s.phi * (kj_at(KJ, r - rg.f_lo).x - kj_at(KJ, r - rg.f_hi - 1).x);
-  if (rg.r_lo <= rg.r_hi) {
-#if TCI_RAMP_PREFIX
-    const double2 hi = kj_at(KJ, r - rg.r_lo), lo = kj_at(KJ, r - rg.r_hi - 1);
-    const double C = hi.x - lo.x;
-    const double Mc = fma(rd, C, -(hi.y - lo.y));  // sum of m * c_{r-m}, exact
-    acc = fma(kvd, Mc, fma(-ka, C, acc));
-#else
-    double kA = kj_at(KJ, r - rg.r_lo).x;
-    for (int m = rg.r_lo; m <= rg.r_hi; ++m) {
-      const double kB = kj_at(KJ, r - m - 1).x;
-      acc = fma(kA - kB, fma((double)m, kvd, -ka), acc);
-      kA = kB;
-    }
-#endif
-  }
-  return acc;
-}
-
-template <int MODE>
-__device__ __forceinline__ void write_nan(int lane, int N, int64_t b, double* out0, double* out1, int64_t ld_out) {
-  if (MODE == MODE_SS) {
-    if (lane == 0) out0[b] = NAN;
-  } else {
-    for (int j = lane; j < N; j += 64) out0[b * ld_out + j] = out1[b * ld_out + j] = NAN;
-  }
-}
-
 template <int RPL, int NSEG, int MODE>
 __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
@@ -198,11 +28,8 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
                                                          double* __restrict__ out0, double* __restrict__ out1,
                                                          int64_t ld_out) {
   constexpr int SLOTS = 64 * RPL;      // rows 1..SLOTS (row 0 never holds a polymerase)
-  // Simulated rows j = 0..SLOTS of each dye: simM[j] = lds[1 + j], simP[j] = lds[SLOTS + 3 + j],
-  // so a lane's first row RPL*lane + 1 starts 16-B aligned (paired 16-B row stores).
-  constexpr int SIMM = 1, SIMP = SLOTS + 3;
   constexpr int NPT = RPL + 1;         // acquisition points per lane (N <= 64*RPL + 1)
-  constexpr int WAVE_DOUBLES = 4 * SLOTS + 4 * RPL;  // {K,J} table (2*SLOTS+RPL entries) / the two sim rows
+  constexpr int WAVE_DOUBLES = eval_lds_doubles<RPL>();  // {K,J} table / the two sim rows
   __shared__ __attribute__((aligned(16))) double s_lds[kWavesPerBlock][WAVE_DOUBLES];
 
   const int lane = threadIdx.x & 63;
@@ -219,9 +46,6 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
   const int64_t b = (int64_t)vb * kWavesPerBlock + wid;
   if (b >= B) return;
   double* lds = s_lds[wid];
-  double* simM = lds + SIMM;
-  double* simP = lds + SIMP;
-  static_assert(SIMP + SLOTS + 1 <= WAVE_DOUBLES, "sim rows exceed the wave's LDS");
 
   // ---- every load of the evaluation is issued here, in one round trip
   const int c = __builtin_amdgcn_readfirstlane(cell_id[b]);
@@ -238,352 +62,36 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
   const StepRec* ST = (MODE == MODE_FWD_RAW ? kp.steps_raw : kp.steps) + cbase;
   const PointRec* PT = kp.points + cbase;
   const double* th = theta + b * ld;
-  const CellMeta cm = kp.cells[c];
-  const double v = th[0], tau = th[1], ton = th[2], b1 = th[3], b2 = th[4], A = th[5], R = th[6];
-  double dr[RPL];
-  StepRec st[RPL];
+  EvalIn<RPL> e;
+  e.cm = kp.cells[c];
+  e.v = th[0];
+  e.tau = th[1];
+  e.ton = th[2];
+  e.b1 = th[3];
+  e.b2 = th[4];
+  e.A = th[5];
+  e.R = th[6];
 #pragma unroll
   for (int q = 0; q < RPL; ++q) {
     const int g = RPL * lane + q;
-    dr[q] = 7 + g < ld ? th[7 + g] : 0.0;  // speculative (N unknown yet), kept inside the row
-    st[q] = ST[g];                          // g < cell_stride
+    e.dr[q] = 7 + g < ld ? th[7 + g] : 0.0;  // speculative (N unknown yet), kept inside the row
+    e.st[q] = ST[g];                          // g < cell_stride
   }
-  PointRec pt[NPT];
-  auto load_points = [&]() {
+  if (MODE != MODE_FWD_RAW) {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int j = lane + 64 * k;
-      if (j <= SLOTS) pt[k] = PT[j];
-      else pt[k] = PointRec{NAN, NAN, NAN, 0, 0};  // beyond every cell's points: dropped
+      if (j <= SLOTS) e.pt[k] = PT[j];
+      else e.pt[k] = PointRec{NAN, NAN, NAN, 0, 0};  // beyond every cell's points: dropped
     }
-  };
-  if (TCI_EARLY_POINTS && MODE != MODE_FWD_RAW) load_points();
-  const int N = cm.n;
+  }
+  const int N = e.cm.n;
   if (ld < 7 + N) {
     write_nan<MODE>(lane, N, b, out0, out1, ld_out);
     return;
   }
-  const int nsteps = N - 1;  // loading steps = rows that can hold polymerases
-#if TCI_ABLATE & 16
-  if (MODE == MODE_SS) {  // memory floor: every load, no compute
-    double x = v + tau + ton + b1 + b2 + A + R + cm.d;
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) x += dr[q] + st[q].dt + st[q].t;
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) x += pt[k].w + pt[k].y1 + pt[k].y2 + (double)pt[k].k;
-    x = lane63(wave_incl_scan(x));
-    if (lane == 0) out0[b] = x;
-    return;
-  }
-#endif
-
-  // ---- per-step setup: R_full = R + dR (SumofSquares...m:45); R<0 -> 0 (ConstantElongationSim.m:36)
-  double prod[RPL];
-  const unsigned ebits = max(max(max(exp_bits(v), exp_bits(tau)), max(exp_bits(ton), exp_bits(b1))),
-                            max(max(exp_bits(b2), exp_bits(A)), exp_bits(R)));
-  const bool fin = ebits != 0x7ff00000u;
-  uint64_t nonfinite = 0;
-#pragma unroll
-  for (int q = 0; q < RPL; ++q) {
-    const int g = RPL * lane + q;
-    const bool valid = g < nsteps;
-    nonfinite |= step_lanes<RPL>(nsteps, q) & wave_ballot(!isfinite(dr[q]));
-    const double rho = fmax(R + dr[q], 0.0);  // R(R<0) = 0 (the sign of a zero cannot reach floor())
-    prod[q] = (valid && !(st[q].t < ton)) ? rho * st[q].dt : 0.0;  // skipped steps add nothing (:57-60)
-  }
-  if (!fin || nonfinite != 0) {  // outside mcmcstat's finite parameter box: reported as NaN
-    write_nan<MODE>(lane, N, b, out0, out1, ld_out);
-    return;
-  }
-
-  // ---- loading counter (ConstantElongationSim.m:60-61): DPP prefix sum + exactness proof
-  double K[RPL];
-  {
-    double loc[RPL];
-    double s = 0.0;
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-      s = s + prod[q];
-      loc[q] = s;
-    }
-#if TCI_ABLATE & 8
-    const double excl = 0.0;
-#else
-    const double excl = wave_shr1(wave_incl_scan(s));
-#endif
-    uint64_t amb = 0;
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) {
-      const double Sq = excl + loc[q];
-      const double eps = Sq * 0x1p-42;  // >> the (g + 16) ulp bound between any two summation orders
-      const double Kq = floor(Sq);
-      amb |= wave_ballot(Sq - eps < Kq) | wave_ballot(Sq + eps >= Kq + 1.0);  // an integer within eps of Sq
-      K[q] = Kq;
-    }
-    if ((kp.force_exact & 1) || amb != 0) {
-      // Exact path: the reference's serial loop, counter = counter + R(i)*dt(i).
-#pragma unroll
-      for (int q = 0; q < RPL; ++q) simM[RPL * lane + q] = prod[q];
-      wave_sync();
-      if (lane == 0) {
-        double counter = 0.0;
-        for (int g = 0; g < nsteps; ++g) {
-          counter = counter + simM[g];
-          simP[g] = floor(counter);
-        }
-      }
-      wave_sync();
-#pragma unroll
-      for (int q = 0; q < RPL; ++q) {
-        const int g = RPL * lane + q;
-        K[q] = simP[min(g, nsteps - 1)];  // constant past the last step, as the scan gives
-      }
-      wave_sync();
-    }
-  }
-
-  SegParams sm[NSEG], sp[NSEG];
-#pragma unroll
-  for (int k = 0; k < NSEG; ++k) {
-    sm[k] = kp.ms2[k];
-    sp[k] = kp.pp7[k];
-  }
-  const double L = kp.L0 + tau * v;                 // L_MS2 = L_PP7 (GetFluorFromPolPos.m:19-20), no FMA
-  const double pstop = L > kp.emax ? L : kp.emax;  // f(p) == 0 for every p >= pstop
-  double accM[NSEG][RPL], accP[NSEG][RPL];
-#pragma unroll
-  for (int q = 0; q < RPL; ++q)
-#pragma unroll
-    for (int k = 0; k < NSEG; ++k) accM[k][q] = accP[k][q] = 0.0;
-
-  // v <= 0: every position stays <= 0 <= loop start, so no polymerase is ever lit.
-  if (v > 0.0) {
-    bool fast = MODE != MODE_FWD_RAW && !(kp.force_exact & 2);
-    const double vd0 = v * cm.d;
-    Regions rgM[NSEG], rgP[NSEG];
-#if TCI_ABLATE & 2
-    if (fast) {
-#pragma unroll
-      for (int k = 0; k < NSEG; ++k) {
-        const int m0 = (int)(sm[k].a / vd0);
-        rgM[k] = Regions{m0 + 1, m0 + 4, m0 + 5, m0 + 20};
-        rgP[k] = Regions{m0 + 9, m0 + 12, m0 + 13, m0 + 20};
-      }
-    }
-    if (false) {
-#else
-    if (fast) {
-#endif
-      // ---- distance regions and their exactness proof
-      // |p(r, r-m) - P_m| <= v * (m*delta + (m+4)*u*m*(d+delta)) for every m <= nsteps; eps is
-      // twice that at m = nsteps, precomputed per cell up to the factor v (CellMeta::eps_v)
-      const double eps = v * cm.eps_v;
-      uint64_t amb = 0;
-      int n_lt_L = 0;
-      // No P_m equals a threshold unless it is within eps > 0 of it (then the wave goes exact),
-      // so on the fast path #(P_m <= x) == #(P_m < x) and one count per threshold suffices.
-      int nM_a[NSEG], nM_e[NSEG], nP_a[NSEG], nP_e[NSEG];
-#pragma unroll
-      for (int k = 0; k < NSEG; ++k) nM_a[k] = nM_e[k] = nP_a[k] = nP_e[k] = 0;
-#pragma unroll
-      for (int q = 0; q < RPL; ++q) {
-        const int g = RPL * lane + q;
-        const uint64_t vmask = step_lanes<RPL>(nsteps, q);  // AND-ed on the scalar unit, not per vote
-        const double md = (double)(g + 1);
-        const double Pm = md * vd0;
-        bool near = fabs(Pm - L) <= eps;
-        n_lt_L += __popcll(vmask & wave_ballot(Pm < L));
-#pragma unroll
-        for (int k = 0; k < NSEG; ++k) {
-          near = near | (fabs(Pm - sm[k].a) <= eps) | (fabs(Pm - sm[k].e) <= eps) | (fabs(Pm - sp[k].a) <= eps) |
-                 (fabs(Pm - sp[k].e) <= eps);
-          nM_a[k] += __popcll(vmask & wave_ballot(Pm < sm[k].a));
-          nM_e[k] += __popcll(vmask & wave_ballot(Pm < sm[k].e));
-          nP_a[k] += __popcll(vmask & wave_ballot(Pm < sp[k].a));
-          nP_e[k] += __popcll(vmask & wave_ballot(Pm < sp[k].e));
-        }
-        amb |= vmask & wave_ballot(near);
-      }
-      fast = amb == 0;
-#pragma unroll
-      for (int k = 0; k < NSEG; ++k) {
-        rgM[k] = Regions{nM_a[k] + 1, nM_e[k], nM_e[k] + 1, n_lt_L};
-        rgP[k] = Regions{nP_a[k] + 1, nP_e[k], nP_e[k] + 1, n_lt_L};
-      }
-    }
-    if (fast) {
-      // ---- {K, J} prefix tables (exact) and O(1) row sums
-      double jloc[RPL], js = 0.0;
-      {
-        const double kprev = wave_shr1(K[RPL - 1]);
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-          const int g = RPL * lane + q;
-          const double cg = K[q] - (q == 0 ? kprev : K[q - 1]);  // 0 past the last step (K constant)
-          js = fma((double)g, cg, js);                           // integers < 2^53: exact
-          jloc[q] = js;
-        }
-      }
-      const double jexcl = wave_shr1(wave_incl_scan(js));
-      // KJ[i], i in [-SLOTS-RPL, SLOTS): the SLOTS+RPL entries below i = 0 are zeros
-      double2* KJ = reinterpret_cast<double2*>(lds) + SLOTS + RPL;
-#pragma unroll
-      for (int q = 0; q < RPL; ++q) {
-        KJ[RPL * lane + q] = make_double2(K[q], jexcl + jloc[q]);
-        KJ[RPL * lane + q - SLOTS - RPL] = make_double2(0.0, 0.0);
-        if (lane == 0) KJ[q - RPL] = make_double2(0.0, 0.0);
-      }
-      wave_sync();
-      double kvdM[NSEG], kaM[NSEG], kvdP[NSEG], kaP[NSEG];
-#pragma unroll
-      for (int k = 0; k < NSEG; ++k) {
-        kvdM[k] = sm[k].k * vd0;
-        kaM[k] = sm[k].k * sm[k].a;
-        kvdP[k] = sp[k].k * vd0;
-        kaP[k] = sp[k].k * sp[k].a;
-      }
-#pragma unroll
-      for (int q = 0; q < RPL; ++q) {
-        const int r = RPL * lane + q + 1;
-        const double rd = (double)r;
-#pragma unroll
-        for (int k = 0; k < NSEG; ++k) {
-#if TCI_ABLATE & 1
-          accM[k][q] = KJ[r].x + (double)rgM[k].f_lo;
-          accP[k][q] = KJ[r].y + (double)rgP[k].f_hi;
-#else
-          accM[k][q] = row_sum(KJ, r, rd, rgM[k], sm[k], kvdM[k], kaM[k]);
-          accP[k][q] = row_sum(KJ, r, rd, rgP[k], sp[k], kvdP[k], kaP[k]);
-#endif
-        }
-      }
-    } else {
-      // ---- exact systolic sweep: at iteration s slot g holds cohort g-s+1 with its forward position
-      double cc[RPL], p[RPL], vd[RPL];
-      {
-        const double kprev = wave_shr1(K[RPL - 1]);
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-          const int g = RPL * lane + q;
-          const double km1 = q == 0 ? kprev : K[q - 1];
-          cc[q] = g < nsteps ? K[q] - km1 : 0.0;
-          p[q] = 0.0;
-          vd[q] = g < nsteps ? v * st[q].dt : 0.0;  // v*dt(i), rounded once (:64)
-        }
-      }
-      for (int s = 1; s <= nsteps; ++s) {
-        if (s > 1) {
-          const double pin = wave_shr1(p[RPL - 1]);
-          const double cin = wave_shr1(cc[RPL - 1]);
-#pragma unroll
-          for (int q = RPL - 1; q >= 1; --q) {
-            p[q] = p[q - 1];
-            cc[q] = cc[q - 1];
-          }
-          p[0] = pin;
-          cc[0] = cin;
-        }
-        uint64_t alive = 0;
-#pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-          p[q] = p[q] + vd[q];  // x(i+1,k) = x(i,k) + v*dt(i)
-#pragma unroll
-          for (int k = 0; k < NSEG; ++k) {
-            accM[k][q] = fma(cc[q], occupancy(p[q], sm[k], L), accM[k][q]);
-            accP[k][q] = fma(cc[q], occupancy(p[q], sp[k], L), accP[k][q]);
-          }
-          alive |= step_lanes<RPL>(nsteps, q) & wave_ballot(cc[q] > 0.0) & wave_ballot(p[q] < pstop);
-        }
-        if (alive == 0) break;
-      }
-    }
-  }
-  wave_sync();  // every {K,J}-table read is done before the rows overwrite the LDS
-
-  // ---- basal floor inside the segment loop (GetFluorFromPolPos.m:54-57,66-69), x A (SumofSquares...m:51)
-  //      Rows past the last step are stored too (never read): stores stay whole 16-B pairs.
-  double rowM[RPL], rowP[RPL];
-#pragma unroll
-  for (int q = 0; q < RPL; ++q) {
-    // MS2(MS2 < basal) = basal == max(MS2, basal): the sums are finite and >= 0 here
-    double m = fmax(accM[0][q], b1), pp = fmax(accP[0][q], b2);
-#pragma unroll
-    for (int k = 1; k < NSEG; ++k) {
-      m = fmax(m + accM[k][q], b1);
-      pp = fmax(pp + accP[k][q], b2);
-    }
-    rowM[q] = A * m;
-    rowP[q] = pp;
-  }
-  if (RPL == 1) {
-    simM[lane + 1] = rowM[0];
-    simP[lane + 1] = rowP[0];
-  } else {
-#pragma unroll
-    for (int q = 0; q < RPL; q += 2) {
-      *reinterpret_cast<double2*>(simM + RPL * lane + q + 1) = make_double2(rowM[q], rowM[q + 1]);
-      *reinterpret_cast<double2*>(simP + RPL * lane + q + 1) = make_double2(rowP[q], rowP[q + 1]);
-    }
-  }
-  if (lane == 0) {  // first row of the reference: no polymerase yet
-    double m = 0.0, pp = 0.0;
-#pragma unroll
-    for (int k = 0; k < NSEG; ++k) {
-      m = m < b1 ? b1 : m;
-      pp = pp < b2 ? b2 : pp;
-    }
-    simM[0] = A * m;
-    simP[0] = pp;
-  }
-  wave_sync();
-
-  if (MODE == MODE_FWD_RAW) {
-    for (int j = lane; j < N; j += 64) {
-      out0[b * ld_out + j] = simM[j];
-      out1[b * ld_out + j] = simP[j];
-    }
-    return;
-  }
-
-  // ---- interp1 back to the acquisition times (SumofSquares...m:55-56) and nansum of the
-  //      squared residuals over [MS2, PP7] (:57-64).
-  if (!TCI_EARLY_POINTS) load_points();
-  double ss = 0.0;
-#if TCI_ABLATE & 4
-  if (MODE == MODE_SS) {
-    ss = simM[lane] + simP[lane] + pt[0].y1 + pt[1].y2;
-    ss = lane63(wave_incl_scan(ss));
-    if (lane == 0) out0[b] = ss;
-    return;
-  }
-#endif
-#pragma unroll
-  for (int kk = 0; kk < NPT; ++kk) {
-    if (kk == RPL && N <= 64 * RPL) break;  // uniform: only N = 64*RPL + 1 has a tail point
-    const int j = lane + 64 * kk;
-    // interp1: NaN outside the grid comes in through w = NaN (PointRec)
-    const int k = pt[kk].k;
-    const double w = pt[kk].w;
-    const double m = fma(w, simM[k + 1] - simM[k], simM[k]);
-    const double pp = fma(w, simP[k + 1] - simP[k], simP[k]);
-    if (MODE == MODE_FWD_INTERP) {
-      if (j < N) {
-        out0[b * ld_out + j] = m;
-        out1[b * ld_out + j] = pp;
-      }
-    } else {
-      // nansum drops NaN data, NaN simulation and the all-NaN padding points (j >= N) alike:
-      // fma(r, r, ss) >= ss unless it is NaN, and max() returns the non-NaN operand.
-      const double r1 = pt[kk].y1 - m;
-      ss = fmax(fma(r1, r1, ss), ss);
-      const double r2 = pt[kk].y2 - pp;
-      ss = fmax(fma(r2, r2, ss), ss);
-    }
-  }
-  if (MODE == MODE_SS) {
-    ss = lane63(wave_incl_scan(ss));
-    if (lane == 0) out0[b] = ss;
-  }
+  const double ss = eval_wave<RPL, NSEG, MODE>(kp, e, lane, lds, b, out0, out1, ld_out);
+  if (MODE == MODE_SS && lane == 0) out0[b] = ss;
 }
 
 template <int RPL, int NSEG, int MODE>
