@@ -156,7 +156,7 @@ typedef struct {
  *            kernel, with its ssfun evaluations in the loop: latency-bound runs (few chains).
  *   BATCHED: one launch per stage, every chain's ssfun in the batched likelihood kernel, replayed
  *            as a hipGraph per adaptation window: many chains, or cells too long for FUSED.
- *   AUTO:    FUSED when every chain fits it (npar <= 520) and there are at most 8 chains per CU. */
+ *   AUTO:    FUSED when its workgroup fits twice in a CU (LDS) and there are at most 8 chains per CU. */
 #define TCI_DRAM_AUTO 0
 #define TCI_DRAM_FUSED 1
 #define TCI_DRAM_BATCHED 2
@@ -173,7 +173,6 @@ typedef struct {
   double* chain;        /* [ceil(n_steps/thin)][n_chains][ld] thinned rows (rows 1, 1+thin, ...) */
   double* s2chain;      /* [ceil(n_steps/thin)][n_chains] */
   double* qcov_R;       /* [n_chains][ld][ld] final proposal factor R (upper): qcov = R'R (mcmcstat results.qcov) */
-  double* qcov_iR;      /* [n_chains][ld][ld] its inverse (upper), used by the delayed-rejection ratio */
   double elapsed_ms;    /* device time of the step loop (HIP events) */
 } tci_dram_outputs;
 

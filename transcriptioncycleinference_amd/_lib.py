@@ -65,7 +65,7 @@ class tci_dram_options(C.Structure):
 class tci_dram_outputs(C.Structure):
     _fields_ = [("mean", _dp), ("std", _dp), ("final_theta", _dp), ("sigma_mean", _dp), ("sigma_std", _dp),
                 ("accept_rate", _dp), ("n_evals", _i64p), ("chain", _dp), ("s2chain", _dp), ("qcov_R", _dp),
-                ("qcov_iR", _dp), ("elapsed_ms", C.c_double)]
+                ("elapsed_ms", C.c_double)]
 
 
 # (name, restype, argtypes) for every symbol declared in include/tci.h

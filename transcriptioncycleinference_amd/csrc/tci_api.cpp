@@ -575,7 +575,6 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(prior, double, n);
   TCI_ALLOC(sigma2, double, n);
   TCI_ALLOC(R, double, n * L2);
-  TCI_ALLOC(iR, double, n * L2);
   TCI_ALLOC(cov, double, n * L2);
   TCI_ALLOC(work, double, n * L2);
   TCI_ALLOC(cmean, double, n * L);
@@ -652,11 +651,15 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   const int64_t ai = opt->adaptint;
   int n_cu = 0;
   TCI_HIP(ctx, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-  const bool fused_fits = tci::dram_chain_lds_bytes(ld, ctx->rpl) <= 64 * 1024;
+  // the fused engine's workgroup keeps the chain's vectors, R (fp32) and two evaluation tables in
+  // LDS: it must fit a CU (160 KB); AUTO also wants two workgroups per CU (<= 80 KB)
+  const int64_t fused_lds = tci::dram_chain_lds_bytes(ld, ctx->rpl);
+  const bool fused_fits = fused_lds <= 160 * 1024;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   bool fused = opt->engine == TCI_DRAM_FUSED;
-  if (opt->engine == TCI_DRAM_AUTO) fused = fused_fits && n_chains <= 8 * (int64_t)std::max(n_cu, 1);
+  if (opt->engine == TCI_DRAM_AUTO)
+    fused = fused_lds <= 80 * 1024 && n_chains <= 8 * (int64_t)std::max(n_cu, 1);
   if (fused && !fused_fits) return fail(ctx, TCI_ERANGE, "tci_dram_run: rows too long for the fused engine");
   if (fused) {
     // Chunks of chain rows up to the next adaptation row; k_chain leaves *st.step at the chunk end.
@@ -747,7 +750,6 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   if (st.chain_out && out->chain)
     TCI_HIP(ctx, hipMemcpy(out->chain, st.chain_out, (size_t)n_keep * n * L * sizeof(double), hipMemcpyDeviceToHost));
   if (out->qcov_R) TCI_HIP(ctx, hipMemcpy(out->qcov_R, st.R, n * L2 * sizeof(double), hipMemcpyDeviceToHost));
-  if (out->qcov_iR) TCI_HIP(ctx, hipMemcpy(out->qcov_iR, st.iR, n * L2 * sizeof(double), hipMemcpyDeviceToHost));
   if (st.s2_out && out->s2chain)
     TCI_HIP(ctx, hipMemcpy(out->s2chain, st.s2_out, (size_t)n_keep * n * sizeof(double), hipMemcpyDeviceToHost));
   return TCI_OK;

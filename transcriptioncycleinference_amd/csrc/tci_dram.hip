@@ -11,13 +11,19 @@
 //   stage 2   (stage 1 rejected) newpar2 = oldpar + randn(1,npar)*R/drscale
 //             alpha32 = min(1, exp(-0.5*(newss-newss2)/sigma2 - 0.5*(newprior-newprior2)))
 //             l2 = exp(-0.5*(newss2-oldss)/sigma2 - 0.5*(newprior2-oldprior))
-//             q1 = exp(-0.5*(|(newpar2-newpar)*iR|^2 - |(oldpar-newpar)*iR|^2))
+//             q1 = exp(-0.5*(|(newpar2-newpar)*iR|^2 - |(oldpar-newpar)*iR|^2)), iR = inv(R)
+//             -- with newpar = oldpar + z1*R and newpar2 = oldpar + z2*R/drscale this is
+//             exp(-0.5*(|z2/drscale - z1|^2 - |z1|^2)) exactly, which is what is evaluated (no iR)
 //             alpha13 = l2*q1*(1-alpha32)/(1-alpha12)
 //   sigma2    1/sigma2 ~ Gamma((N0+N)/2, scale 2/(N0*S20 + oldss)), N0 = 0, N = length(ydata)
 //   adapt     every adaptint steps: burn-in (step < burnintime): R scaled by 1/burnin_scale or
 //             burnin_scale when the window's rejection rate is > 0.95 or < 0.05; afterwards
 //             covupd over all chain rows so far, R = chol(cov + qcovadj*I) * adascale
 //   prior     sum(((theta - mu)./sig).^2) over parameters with finite sig (dR: N(0, 50), :254)
+// The proposal factor R is kept with float-representable entries (rounded once when it is set),
+// so a chain's R fits in LDS as fp32 (P(P+1)/2 floats) for the proposal products; the proposal
+// covariance is then R'R of that rounded R, consistently in both stages (a 1e-7-relative change
+// of the proposal shape; the sampler stays exact for it).
 // Randomness: Philox4x32-10 keyed by (seed), counter (chain, step, purpose, index) -- the
 // stream is reproducible and independent of launch geometry (MATLAB's MT19937 is not
 // reproducible here, so chain parity with the reference is statistical only).
@@ -34,6 +40,8 @@
 namespace tci {
 
 namespace {
+
+constexpr int kThreads = 256;  // one workgroup (4 waves) per chain
 
 enum Purpose : uint32_t { P_NORM1 = 1, P_U1 = 2, P_NORM2 = 3, P_U2 = 4, P_GAMMA = 5 };
 
@@ -66,12 +74,22 @@ __device__ __forceinline__ double u01(uint32_t a, uint32_t b) {
   return ((double)x + 0.5) * 0x1p-53;
 }
 
-// Standard normal number `j` of the stream (chain, step, purpose): Box-Muller on pairs.
-__device__ __forceinline__ double normal_at(uint64_t seed, int64_t c, int64_t step, uint32_t purpose, int j) {
-  const uint4 r = rng(seed, c, step, purpose, (uint32_t)(j >> 1));
+// Standard normals 2*pair and 2*pair+1 of the stream (chain, step, purpose): Box-Muller.
+__device__ __forceinline__ double2 normal_pair(uint64_t seed, int64_t c, int64_t step, uint32_t purpose, int pair) {
+  const uint4 r = rng(seed, c, step, purpose, (uint32_t)pair);
   const double u1 = u01(r.x, r.y), u2 = u01(r.z, r.w);
   const double rad = sqrt(-2.0 * log(u1));
-  return (j & 1) ? rad * sin(2.0 * M_PI * u2) : rad * cos(2.0 * M_PI * u2);
+  return make_double2(rad * cos(2.0 * M_PI * u2), rad * sin(2.0 * M_PI * u2));
+}
+
+// z[0..P) of stream `purpose` into LDS, one Box-Muller pair per thread and round.
+__device__ __forceinline__ void draw_normals(uint64_t seed, int64_t c, int64_t step, uint32_t purpose, int P,
+                                             double* z, int t) {
+  for (int q = t; 2 * q < P; q += kThreads) {
+    const double2 n = normal_pair(seed, c, step, purpose, q);
+    z[2 * q] = n.x;
+    if (2 * q + 1 < P) z[2 * q + 1] = n.y;
+  }
 }
 
 __device__ __forceinline__ double uniform_at(uint64_t seed, int64_t c, int64_t step, uint32_t purpose) {
@@ -91,7 +109,9 @@ __device__ double gamma_at(uint64_t seed, int64_t c, int64_t step, double a, dou
     double v = 1.0 + cc * x;
     if (v <= 0.0) continue;
     v = v * v * v;
-    if (log(u) < 0.5 * x * x + d - d * v + d * log(v)) return d * v * scale;
+    const double x2 = x * x;
+    if (u < 1.0 - 0.0331 * x2 * x2) return d * v * scale;  // squeeze (implies the log test)
+    if (log(u) < 0.5 * x2 + d - d * v + d * log(v)) return d * v * scale;
   }
   return a * scale;  // unreachable in practice (acceptance > 0.95 per try)
 }
@@ -102,8 +122,33 @@ __device__ __forceinline__ double wsum64(double x) {
   return x;
 }
 
-constexpr int kThreads = 256;  // one workgroup (4 waves) per chain
 constexpr int kVec = TCI_MAX_POINTS + 8;
+
+// Prior SS sum(((th - mu)./sig).^2) over finite sig (mcmcstat's default priorfun) by ONE wave:
+// lane l sums j = l, l + 64, .. in order, then a fixed xor-shuffle tree. Both engines call this,
+// so the bits agree.
+__device__ double wave_prior(const double* th, const double* mu, const double* sig, int P, int lane) {
+  double s = 0.0;
+  for (int j = lane; j < P; j += 64) {
+    const double sg = sig[j];
+    if (isfinite(sg)) {
+      const double z = (th[j] - mu[j]) / sg;
+      s += z * z;
+    }
+  }
+  return wsum64(s);
+}
+
+// |z2/drscale - z1|^2 and |z1|^2 (the delayed-rejection ratio, header) by ONE wave.
+__device__ double2 wave_q(const double* z1, const double* z2, double inv_ds, int P, int lane) {
+  double q21 = 0.0, q01 = 0.0;
+  for (int j = lane; j < P; j += 64) {
+    const double d = z2[j] * inv_ds - z1[j];
+    q21 += d * d;
+    q01 += z1[j] * z1[j];
+  }
+  return make_double2(wsum64(q21), wsum64(q01));
+}
 
 // Workgroup sum (all threads get the result). red: LDS scratch of >= 4 doubles.
 __device__ double block_sum(double x, double* red) {
@@ -130,71 +175,110 @@ __device__ double prior_ss(const double* th, const double* mu, const double* sig
   return block_sum(s, red);
 }
 
-// Row-vector times upper-triangular matrix, out_j = sum_{i<=j} v_i M[i][j] (M row-major, stride
-// ld, in global memory), for up to two vectors sharing each load of M. Wave w takes the rows
-// i == w (mod 4) (balanced over the triangle); lanes take columns; 8 loads in flight per lane.
-// v0/v1 and the outputs are in LDS; part = LDS [2][4][ps] (ps >= P).
-template <int NV>
-__device__ void tri_vecmat(const double* v0, const double* v1, const double* M, int64_t ld, int P, double* part,
-                           double* out0, double* out1, int ps = kVec) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int j0 = 0; j0 < P; j0 += 64) {
-    const int j = j0 + lane;
-    const int imax = (j0 + 63 < P - 1 ? j0 + 63 : P - 1);  // uniform
-    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-    int i = w;
-    for (; i + 28 <= imax; i += 32) {
-      double r[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int ii = i + 4 * u;
-        r[u] = (ii <= j && j < P) ? M[(int64_t)ii * ld + j] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u += 2) {
-        a0 = fma(v0[i + 4 * u], r[u], a0);
-        a1 = fma(v0[i + 4 * u + 4], r[u + 1], a1);
-        if (NV == 2) {
-          b0 = fma(v1[i + 4 * u], r[u], b0);
-          b1 = fma(v1[i + 4 * u + 4], r[u + 1], b1);
-        }
-      }
-    }
-    for (; i <= imax; i += 4) {
-      const double r = (i <= j && j < P) ? M[(int64_t)i * ld + j] : 0.0;
-      a0 = fma(v0[i], r, a0);
-      if (NV == 2) b0 = fma(v1[i], r, b0);
+// Proposal factor entries are kept float-representable (see the header).
+__device__ __forceinline__ double f32_round(double x) { return (double)(float)x; }
+
+// Packed upper triangle (row i at i*P - i*(i-1)/2) of a chain's R as fp32 in LDS.
+__device__ __forceinline__ int tri_off(int i, int P) { return i * P - (i * (i - 1)) / 2; }
+__device__ void load_R_f32(float* Rl, const double* R, int64_t ld, int P) {
+  for (int i = 0; i < P; ++i) {
+    const int oi = tri_off(i, P);
+    for (int j = i + (int)threadIdx.x; j < P; j += kThreads) Rl[oi + j - i] = (float)R[(int64_t)i * ld + j];
+  }
+}
+
+// Proposal products U[r][j] = sum_{i<=j} Z[r][i] R[i][j] for r < M <= 16 rows of normals (LDS,
+// row stride zs) and the chain's packed fp32 R (LDS), written to U (LDS, row stride us). One
+// v_mfma_f64_16x16x4_f64 per 4-row k-step of a 16-column tile: A = Z[row = lane&15][k = lane>>4],
+// B = R[k = lane>>4][col = lane&15], D row = (lane>>4) + 4 r, col = lane&15 (cdna_hip_programming.md
+// f64 MFMA map). Tiles skip the k-steps below the triangle; a row's result depends only on that row
+// and the fixed k order, so the fused engine (8 rows: 4 steps x 2 stages) and the per-stage kernels
+// (1 row) produce identical bits. Column tiles go to the 4 waves in snake order (balanced costs).
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+__device__ void mfma_zr(const double* Z, int zs, int M, const float* Rl, int P, double* U, int us) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int row = lane & 15, kq = lane >> 4;
+  const int ntiles = (P + 15) >> 4;
+  const int zr = (row < M ? row : M - 1) * zs;  // clamped: rows >= M read row M-1, zeroed below
+  for (int g = 0; 4 * g < ntiles; ++g) {
+    const int nt = 4 * g + ((g & 1) ? 3 - w : w);  // uniform
+    if (nt >= ntiles) continue;
+    const int j = 16 * nt + row;
+    const int jc = j < P ? j : P - 1;
+    const int kmax = min(16 * nt + 15, P - 1);  // uniform: the last row reaching this tile
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int i0 = 0; i0 <= kmax; i0 += 4) {
+      const int i = i0 + kq;
+      const int ic = i < P ? i : P - 1;
+      const double zv = Z[zr + ic];
+      const float rv = Rl[tri_off(ic, P) + (jc >= ic ? jc - ic : 0)];
+      const double a = (row < M && i < P) ? zv : 0.0;
+      const double b = (i <= j && j < P) ? (double)rv : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
     }
     if (j < P) {
-      part[(0 * 4 + w) * ps + j] = a0 + a1;
-      if (NV == 2) part[(1 * 4 + w) * ps + j] = b0 + b1;
+      if (kq < M) U[kq * us + j] = acc[0];
+      if (kq + 4 < M) U[(kq + 4) * us + j] = acc[1];
+      if (kq + 8 < M) U[(kq + 8) * us + j] = acc[2];
+      if (kq + 12 < M) U[(kq + 12) * us + j] = acc[3];
     }
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < P; j += kThreads) {
-    out0[j] = (part[0 * ps + j] + part[1 * ps + j]) + (part[2 * ps + j] + part[3 * ps + j]);
-    if (NV == 2) out1[j] = (part[4 * ps + j] + part[5 * ps + j]) + (part[6 * ps + j] + part[7 * ps + j]);
   }
   __syncthreads();
 }
 
+// Dynamic LDS of the per-stage kernels (vector stride L = ld >= P): z, y, red and the chain's R
+// as packed fp32.
 struct Smem {
-  double z[kVec];
-  double y[kVec];
-  double d0[kVec];
-  double d1[kVec];
-  double part[8 * kVec];
-  double red[8];
-  int flag;
+  double* z;
+  double* y;
+  double* red;
+  float* Rl;
+  int L;
 };
+__host__ __device__ inline int64_t stage_lds_bytes(int64_t L) { return (2 * L + 8) * 8 + (L * (L + 1) / 2) * 4 + 16; }
+__device__ __forceinline__ Smem stage_smem(double* dyn, int L) {
+  Smem m;
+  m.z = dyn;
+  m.y = dyn + L;
+  m.red = dyn + 2 * L;
+  m.Rl = reinterpret_cast<float*>(dyn + 2 * L + 8);
+  m.L = L;
+  return m;
+}
+
+// Delayed-rejection proposal ratio q1 = exp(-0.5*(|(y2-y1) iR|^2 - |(x-y1) iR|^2)) from the
+// normals: (y2-y1) iR = z2/drscale - z1 and (x-y1) iR = -z1 (z1, z2 in LDS).
+__device__ double dr_q1(const double* z1, const double* z2, double inv_ds, int P, double* red) {
+  if (threadIdx.x < 64) {
+    const double2 q = wave_q(z1, z2, inv_ds, P, threadIdx.x);
+    if (threadIdx.x == 0) red[0] = exp(-0.5 * (q.x - q.y));
+  }
+  __syncthreads();
+  const double q1 = red[0];
+  __syncthreads();
+  return q1;
+}
+
+// Prior SS (wave_prior by wave 0), broadcast to the block.
+__device__ double prior_block(const double* th, const double* mu, const double* sig, int P, double* red) {
+  if (threadIdx.x < 64) {
+    const double v = wave_prior(th, mu, sig, P, threadIdx.x);
+    if (threadIdx.x == 0) red[0] = v;
+  }
+  __syncthreads();
+  const double v = red[0];
+  __syncthreads();
+  return v;
+}
 
 // Draw z (stream `purpose`), y = base + scale * z*R into LDS and global `out`; returns in-bounds.
 __device__ bool propose_block(const DramState& st, const DramParams& p, int64_t c, int64_t step, uint32_t purpose,
                               const double* base, double scale, int P, double* out, Smem& sm) {
   const int64_t ld = st.ld;
-  for (int j = threadIdx.x; j < P; j += kThreads) sm.z[j] = normal_at(p.seed, c, step, purpose, j);
+  draw_normals(p.seed, c, step, purpose, P, sm.z, threadIdx.x);
+  load_R_f32(sm.Rl, st.R + c * ld * ld, ld, P);
   __syncthreads();
-  tri_vecmat<1>(sm.z, nullptr, st.R + c * ld * ld, ld, P, sm.part, sm.y, nullptr);
+  mfma_zr(sm.z, sm.L, 1, sm.Rl, P, sm.y, sm.L);
   int inb = 1;
   for (int j = threadIdx.x; j < P; j += kThreads) {
     const double v = base[j] + scale * sm.y[j];
@@ -213,18 +297,14 @@ __global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* _
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   double* R = st.R + c * ld * ld;
-  double* iR = st.iR + c * ld * ld;
   double* cv = st.cov + c * ld * ld;
   for (int64_t e = threadIdx.x; e < ld * ld; e += kThreads) {
     R[e] = 0.0;
-    iR[e] = 0.0;
     cv[e] = 0.0;
   }
   __syncthreads();
   for (int j = threadIdx.x; j < P; j += kThreads) {
-    const double sd = sqrt(qdiag[c * ld + j]);  // R = chol(qcov), qcov = J0 diagonal (:230)
-    R[(int64_t)j * ld + j] = sd;
-    iR[(int64_t)j * ld + j] = 1.0 / sd;
+    R[(int64_t)j * ld + j] = f32_round(sqrt(qdiag[c * ld + j]));  // R = chol(qcov), qcov = J0 diagonal (:230)
     st.cmean[c * ld + j] = 0.0;
   }
   const double pr = prior_ss(st.theta + c * ld, st.pmu + c * ld, st.psig + c * ld, P, red);
@@ -238,40 +318,60 @@ __global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* _
   }
 }
 
-// Chain row `row` (1-based) = the current state th (global or LDS) with error variance s2:
-// covupd window, posterior stats, thinned output.
-__device__ void record_row(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P, const double* th,
-                           double s2) {
+// Chain row `row` (1-based) = the current state th (global or LDS): the covupd window row, the
+// posterior Welford stats (mean/M2 arrays in global or LDS) and the thinned output row; entries
+// j = j0, j0 + js, .. of the row.
+__device__ void record_vec(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P, const double* th,
+                           double* smean, double* sm2, int j0, int js) {
   const int64_t ld = st.ld;
-  const int t = threadIdx.x;
   if (p.adaptint > 0) {
     double* w = st.window + (c * p.adaptint + (row - 1) % p.adaptint) * ld;
-    for (int j = t; j < P; j += kThreads) w[j] = th[j];
+    for (int j = j0; j < P; j += js) w[j] = th[j];
   }
   if (row >= p.stats_from) {  // posterior mean / population std over chain(stats_from:end, :) (:276-301)
     const double n = (double)(row - p.stats_from + 1);
-    for (int j = t; j < P; j += kThreads) {
+    for (int j = j0; j < P; j += js) {
       const double x = th[j];
-      double m = st.smean[c * ld + j];
+      double m = smean[j];
       const double d = x - m;
       m += d / n;
-      st.smean[c * ld + j] = m;
-      st.sm2[c * ld + j] += d * (x - m);
+      smean[j] = m;
+      sm2[j] += d * (x - m);
     }
-  }
-  if (t == 0) {  // s2 statistics over the whole s2chain (:302-303)
-    st.s2sum[c] += s2;
-    const double q = sqrt(s2), n = (double)row;
-    const double d = q - st.sq_mean[c];
-    st.sq_mean[c] += d / n;
-    st.sq_m2[c] += d * (q - st.sq_mean[c]);
   }
   if (st.chain_out != nullptr && p.thin > 0 && (row - 1) % p.thin == 0) {
     const int64_t k = (row - 1) / p.thin;
-    if (k < p.n_keep) {
-      for (int j = t; j < P; j += kThreads) st.chain_out[(k * st.n_chains + c) * ld + j] = th[j];
-      if (t == 0 && st.s2_out) st.s2_out[k * st.n_chains + c] = s2;
-    }
+    if (k < p.n_keep)
+      for (int j = j0; j < P; j += js) st.chain_out[(k * st.n_chains + c) * ld + j] = th[j];
+  }
+}
+
+// The s2 statistics of chain row `row` over the whole s2chain (:302-303) and its thinned s2.
+struct S2Stats {
+  double sum, qmean, qm2;
+};
+__device__ void record_s2(const DramState& st, const DramParams& p, int64_t c, int64_t row, double s2, S2Stats& a) {
+  a.sum += s2;
+  const double q = sqrt(s2), n = (double)row;
+  const double d = q - a.qmean;
+  a.qmean += d / n;
+  a.qm2 += d * (q - a.qmean);
+  if (st.s2_out != nullptr && p.thin > 0 && (row - 1) % p.thin == 0) {
+    const int64_t k = (row - 1) / p.thin;
+    if (k < p.n_keep) st.s2_out[k * st.n_chains + c] = s2;
+  }
+}
+
+// Both parts for the per-stage kernels (global stats).
+__device__ void record_row(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P, const double* th,
+                           double s2) {
+  record_vec(st, p, c, row, P, th, st.smean + c * st.ld, st.sm2 + c * st.ld, threadIdx.x, kThreads);
+  if (threadIdx.x == 0) {
+    S2Stats a{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
+    record_s2(st, p, c, row, s2, a);
+    st.s2sum[c] = a.sum;
+    st.sq_mean[c] = a.qmean;
+    st.sq_m2[c] = a.qm2;
   }
 }
 
@@ -293,7 +393,8 @@ __global__ __launch_bounds__(kThreads) void k_init_stats(DramState st, DramParam
 }
 
 __global__ __launch_bounds__(kThreads) void k_propose1(DramState st, DramParams p) {
-  __shared__ Smem sm;
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  Smem sm = stage_smem(dyn, (int)st.ld);
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int64_t step = *st.step;
@@ -307,7 +408,8 @@ __global__ __launch_bounds__(kThreads) void k_propose1(DramState st, DramParams 
 }
 
 __global__ __launch_bounds__(kThreads) void k_accept1(DramState st, DramParams p) {
-  __shared__ Smem sm;
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  Smem sm = stage_smem(dyn, (int)st.ld);
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int64_t step = *st.step;
@@ -319,7 +421,7 @@ __global__ __launch_bounds__(kThreads) void k_accept1(DramState st, DramParams p
   double a12 = 0.0, pr1 = 0.0;
   bool acc = false;
   if (inb) {
-    pr1 = prior_ss(y1, st.pmu + c * ld, st.psig + c * ld, P, sm.red);
+    pr1 = prior_block(y1, st.pmu + c * ld, st.psig + c * ld, P, sm.red);
     const double e = -0.5 * (st.ss1[c] - st.ss[c]) / st.sigma2[c] - 0.5 * (pr1 - st.prior[c]);
     a12 = fmin(1.0, exp(e));
     acc = uniform_at(p.seed, c, step, P_U1) < a12;
@@ -346,7 +448,8 @@ __global__ __launch_bounds__(kThreads) void k_accept1(DramState st, DramParams p
 }
 
 __global__ __launch_bounds__(kThreads) void k_accept2(DramState st, DramParams p) {
-  __shared__ Smem sm;
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  Smem sm = stage_smem(dyn, (int)st.ld);
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int64_t step = *st.step;
@@ -355,27 +458,16 @@ __global__ __launch_bounds__(kThreads) void k_accept2(DramState st, DramParams p
   double* th = st.theta + c * ld;
   bool acc2 = false;
   if (p.ntry >= 2 && st.act2[c] != 0) {  // stage 2 was proposed (stage 1 rejected) and is in bounds
-    const double* y1 = st.prop1 + c * ld;
     const double* y2 = st.prop2 + c * ld;
-    const double pr2 = prior_ss(y2, st.pmu + c * ld, st.psig + c * ld, P, sm.red);
+    const double pr2 = prior_block(y2, st.pmu + c * ld, st.psig + c * ld, P, sm.red);
     const double s2 = st.sigma2[c], ss2 = st.ss2[c], ss1 = st.ss1[c], a12 = st.a12[c];
     // ss1 = +Inf (stage 1 out of bounds) gives alpha32 = 0, alpha12 = 0
     const double a32 = fmin(1.0, exp(-0.5 * (ss1 - ss2) / s2 - 0.5 * (st.prior1[c] - pr2)));
     const double l2 = exp(-0.5 * (ss2 - st.ss[c]) / s2 - 0.5 * (pr2 - st.prior[c]));
-    for (int j = threadIdx.x; j < P; j += kThreads) {
-      sm.d1[j] = y2[j] - y1[j];
-      sm.d0[j] = th[j] - y1[j];
-    }
+    draw_normals(p.seed, c, step, P_NORM1, P, sm.z, threadIdx.x);
+    draw_normals(p.seed, c, step, P_NORM2, P, sm.y, threadIdx.x);
     __syncthreads();
-    tri_vecmat<2>(sm.d1, sm.d0, st.iR + c * ld * ld, ld, P, sm.part, sm.z, sm.y);
-    double q21 = 0.0, q01 = 0.0;
-    for (int j = threadIdx.x; j < P; j += kThreads) {
-      q21 += sm.z[j] * sm.z[j];
-      q01 += sm.y[j] * sm.y[j];
-    }
-    q21 = block_sum(q21, sm.red);
-    q01 = block_sum(q01, sm.red);
-    const double q1 = exp(-0.5 * (q21 - q01));  // |(y2-y1) iR|^2 - |(x-y1) iR|^2
+    const double q1 = dr_q1(sm.z, sm.y, 1.0 / p.drscale, P, sm.red);
     const double a13 = l2 * q1 * (1.0 - a32) / (1.0 - a12);
     acc2 = uniform_at(p.seed, c, step, P_U2) < a13;
     if (acc2) {
@@ -416,7 +508,6 @@ __global__ __launch_bounds__(kThreads) void k_adapt(DramState st, DramParams p) 
   double* cvg = st.cov + c * ld * ld;
   double* mu = st.cmean + c * ld;
   double* R = st.R + c * ld * ld;
-  double* iR = st.iR + c * ld * ld;
   const bool in_lds = p.lds_matrix != 0;
   double* A = in_lds ? dyn : st.work + c * ld * ld;
   const int64_t lda = in_lds ? P : ld;
@@ -466,8 +557,7 @@ __global__ __launch_bounds__(kThreads) void k_adapt(DramState st, DramParams p) 
     if (s != 1.0) {
       for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
         const int i = (int)(e / P), j = (int)(e % P);
-        R[(int64_t)i * ld + j] *= s;
-        iR[(int64_t)i * ld + j] /= s;
+        R[(int64_t)i * ld + j] = f32_round(R[(int64_t)i * ld + j] * s);
       }
     }
     __syncthreads();
@@ -500,27 +590,7 @@ __global__ __launch_bounds__(kThreads) void k_adapt(DramState st, DramParams p) 
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
     for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
       const int i = (int)(e / P), j = (int)(e % P);
-      const double r = j >= i ? A[(int64_t)i * lda + j] * sc : 0.0;
-      A[(int64_t)i * lda + j] = r;  // A now holds R (upper), lower part zero
-      R[(int64_t)i * ld + j] = r;
-    }
-    __syncthreads();
-    // iR = R \ I, in place on A, row by row from the bottom: X(i,j) = (d_ij - sum_{k=i+1..j} R(i,k) X(k,j)) / R(i,i)
-    for (int i = P - 1; i >= 0; --i) {
-      const double rii = A[(int64_t)i * lda + i];
-      // row i of R (k > i) is read before being overwritten by row i of X: stage it
-      for (int k = i + 1 + t; k < P; k += kThreads) xs[k] = A[(int64_t)i * lda + k];
-      __syncthreads();
-      for (int j = i + t; j < P; j += kThreads) {
-        double s = (i == j) ? 1.0 : 0.0;
-        for (int k = i + 1; k <= j; ++k) s -= xs[k] * A[(int64_t)k * lda + j];
-        A[(int64_t)i * lda + j] = s / rii;
-      }
-      __syncthreads();
-    }
-    for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
-      const int i = (int)(e / P), j = (int)(e % P);
-      iR[(int64_t)i * ld + j] = j >= i ? A[(int64_t)i * lda + j] : 0.0;
+      R[(int64_t)i * ld + j] = j >= i ? f32_round(A[(int64_t)i * lda + j] * sc) : 0.0;
     }
   }
   __syncthreads();
@@ -534,19 +604,6 @@ __global__ __launch_bounds__(kThreads) void k_adapt(DramState st, DramParams p) 
 // and used only when stage 1 rejects, so nothing changes but the latency). Adaptation stays the
 // k_adapt launch between chunks. Same RNG keys, reductions and operation order as the batched
 // engine above: the two engines produce identical chains (tests/test_dram_gpu.py).
-
-// Prior SS from LDS copies of mu / sig (same arithmetic as prior_ss).
-__device__ double prior_lds(const double* th, const double* mu, const double* sig, int P, double* red) {
-  double s = 0.0;
-  for (int j = threadIdx.x; j < P; j += kThreads) {
-    const double sg = sig[j];
-    if (isfinite(sg)) {
-      const double z = (th[j] - mu[j]) / sg;
-      s += z * z;
-    }
-  }
-  return block_sum(s, red);
-}
 
 #ifndef TCI_CHAIN_PROFILE
 #define TCI_CHAIN_PROFILE 0  // diagnostics: per-phase s_memtime cycles of k_chain into st.prof
@@ -563,8 +620,35 @@ __device__ __forceinline__ uint64_t stamp() {
 #endif
 }
 
-// Dynamic LDS doubles of k_chain for vector stride L (>= P): 11 vectors, 8 partial rows, red.
-__host__ __device__ inline int64_t chain_lds_doubles(int64_t L) { return 19 * L + 8; }
+// Steps per proposal block of k_chain: the normals of kBlockSteps steps (2 stages each: 8 rows)
+// are drawn together and multiplied by R in one pass of MFMA tiles.
+constexpr int kBlockSteps = 4;
+
+// Dynamic LDS bytes of k_chain for vector stride L (>= P): 9 vectors, the block's normals and
+// products (2 x 8 rows), red, and the chain's R as packed fp32 (constant over a chunk).
+__host__ __device__ inline int64_t chain_lds_bytes(int64_t L) {
+  return (9 * L + 4 * kBlockSteps * L + 8) * 8 + (L * (L + 1) / 2) * 4 + 16;
+}
+
+// Normals of both stages for `ns` steps from `step` into rows 2 k (stage 1, P_NORM1) and 2 k + 1
+// (stage 2, P_NORM2) of Z (row stride L), one Box-Muller pair per thread and round.
+__device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int64_t step, int ns, int P, bool two,
+                                                   double* Z, int L) {
+  const int np = (P + 1) / 2;
+  const int rows = 2 * ns;
+  for (int k = threadIdx.x; k < rows * np; k += kThreads) {
+    const int r = k / np, q = k - r * np;
+    double* z = Z + r * L;
+    if ((r & 1) && !two) {
+      z[2 * q] = 0.0;
+      if (2 * q + 1 < P) z[2 * q + 1] = 0.0;
+      continue;
+    }
+    const double2 n = normal_pair(seed, c, step + (r >> 1), (r & 1) ? P_NORM2 : P_NORM1, q);
+    z[2 * q] = n.x;
+    if (2 * q + 1 < P) z[2 * q + 1] = n.y;
+  }
+}
 
 template <int RPL, int NSEG>
 __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
@@ -579,25 +663,28 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   const int64_t ld = st.ld;
   const int L = (int)ld;
   const int P = st.npar[c];
-  double* z = dyn;
-  double* y = z + L;
-  double* d0 = y + L;
-  double* d1 = d0 + L;
-  double* y1 = d1 + L;
+  double* y1 = dyn;
   double* y2 = y1 + L;
   double* th = y2 + L;
   double* lo = th + L;
   double* hi = lo + L;
   double* mu = hi + L;
   double* sg = mu + L;
-  double* part = sg + L;
-  double* red = part + 8 * L;
+  double* smn = sg + L;                     // posterior Welford mean / M2 of the chain (this chunk)
+  double* sm2 = smn + L;
+  double* Zb = sm2 + L;                     // 2*kBlockSteps normal rows (stage 1, stage 2 per step)
+  double* Ub = Zb + 2 * kBlockSteps * L;    // their products with R
+  double* red = Ub + 2 * kBlockSteps * L;   // [0..3]: prior1, prior2, q21, q01; [4]: sigma2
+  float* Rl = reinterpret_cast<float*>(red + 8);
+  load_R_f32(Rl, st.R + c * ld * ld, ld, P);
   for (int j = t; j < P; j += kThreads) {
     th[j] = st.theta[c * ld + j];
     lo[j] = st.lower[c * ld + j];
     hi[j] = st.upper[c * ld + j];
     mu[j] = st.pmu[c * ld + j];
     sg[j] = st.psig[c * ld + j];
+    smn[j] = st.smean[c * ld + j];
+    sm2[j] = st.sm2[c * ld + j];
   }
   // the chain's cell records stay in the registers of the two evaluating waves
   EvalIn<RPL> e;
@@ -614,11 +701,11 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     }
   }
   double ss = st.ss[c], prior = st.prior[c], s2 = st.sigma2[c];
+  S2Stats s2a{0.0, 0.0, 0.0};  // held by wave 3
+  if (w == 3) s2a = S2Stats{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
   int32_t nacc = st.naccept[c], nrej = st.nrej_win[c];
   int64_t nev = st.nevals[c];
   const double half_nobs = 0.5 * (double)st.nobs[c];
-  const double* Rm = st.R + c * ld * ld;
-  const double* iRm = st.iR + c * ld * ld;
   const double scale2 = 1.0 / p.drscale;
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t t0 = stamp(), t1;
@@ -626,19 +713,25 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   if (TCI_CHAIN_PROFILE) { t1 = stamp(); ph[k] += t1 - t0; t0 = t1; }
   __syncthreads();
   for (int64_t step = s_begin; step <= s_end; ++step) {
-    // ---- proposals: stage 1 theta + z1*R, stage 2 theta + z2*R/drscale (both drawn now)
-    for (int j = t; j < P; j += kThreads) {
-      z[j] = normal_at(p.seed, c, step, P_NORM1, j);
-      d0[j] = p.ntry >= 2 ? normal_at(p.seed, c, step, P_NORM2, j) : 0.0;
+    // ---- proposals: stage 1 theta + z1*R, stage 2 theta + z2*R/drscale (both drawn up front,
+    //      kBlockSteps steps at a time: the products are state-independent)
+    const int sl = (int)((step - s_begin) % kBlockSteps);
+    if (sl == 0) {
+      const int ns = (int)min<int64_t>(kBlockSteps, s_end - step + 1);
+      draw_block_normals(p.seed, c, step, ns, P, p.ntry >= 2, Zb, L);
+      __syncthreads();
+      TCI_PHASE(0)
+      mfma_zr(Zb, L, 2 * ns, Rl, P, Ub, L);
+      TCI_PHASE(1)
     }
-    __syncthreads();
-    TCI_PHASE(0)
-    tri_vecmat<2>(z, d0, Rm, ld, P, part, y, d1, L);
-    TCI_PHASE(1)
+    const double* z1 = Zb + (2 * sl) * L;
+    const double* z2 = Zb + (2 * sl + 1) * L;
+    const double* u1 = Ub + (2 * sl) * L;
+    const double* u2 = Ub + (2 * sl + 1) * L;
     int ok1 = 1, ok2 = 1;
     for (int j = t; j < P; j += kThreads) {
-      const double a = th[j] + 1.0 * y[j];
-      const double b = th[j] + scale2 * d1[j];
+      const double a = th[j] + 1.0 * u1[j];
+      const double b = th[j] + scale2 * u2[j];
       y1[j] = a;
       y2[j] = b;
       ok1 &= (a >= lo[j] && a <= hi[j]) ? 1 : 0;
@@ -647,7 +740,9 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     const bool inb1 = __syncthreads_and(ok1) != 0;
     const bool inb2 = __syncthreads_and(ok2) != 0 && p.ntry >= 2;
     TCI_PHASE(2)
-    // ---- ssfun of both proposals, one wavefront each (out of bounds: not called, +Inf)
+    // ---- one phase, four waves: ssfun of both proposals (waves 0, 1; out of bounds: not called,
+    //      +Inf); priors and the delayed-rejection sums (wave 2); the previous row's record and
+    //      sigma2 Gibbs draw (waves 2, 3; sigma2 is first used by this step's acceptance).
     if (w < 2) {
       const double* yy = w == 0 ? y1 : y2;
       double r = INFINITY;
@@ -667,65 +762,76 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
         r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
       }
       if (lane == 0) ssv[w] = r;
+    } else if (w == 2) {
+      const double pr1 = wave_prior(y1, mu, sg, P, lane);
+      const double pr2 = wave_prior(y2, mu, sg, P, lane);
+      const double2 q = wave_q(z1, z2, scale2, P, lane);
+      if (lane == 0) {
+        red[0] = pr1;
+        red[1] = pr2;
+        red[2] = q.x;
+        red[3] = q.y;
+      }
+      if (step > s_begin) record_vec(st, p, c, step - 1, P, th, smn, sm2, lane, 64);
+    } else {
+      if (step > s_begin) {
+        if (p.updatesigma) s2 = 1.0 / gamma_at(p.seed, c, step - 1, half_nobs, 2.0 / ss);
+        if (lane == 0) record_s2(st, p, c, step - 1, s2, s2a);
+      }
+      if (lane == 0) red[4] = s2;
     }
     __syncthreads();
     TCI_PHASE(3)
     const double ss1 = ssv[0], ss2 = ssv[1];
+    s2 = red[4];
     // ---- stage 1 (k_accept1)
     double a12 = 0.0, pr1 = 0.0;
     bool acc = false;
     if (inb1) {
       nev += 1;
-      pr1 = prior_lds(y1, mu, sg, P, red);
+      pr1 = red[0];
       const double ex = -0.5 * (ss1 - ss) / s2 - 0.5 * (pr1 - prior);
       a12 = fmin(1.0, exp(ex));
       acc = uniform_at(p.seed, c, step, P_U1) < a12;
     }
-    if (acc) {
-      for (int j = t; j < P; j += kThreads) th[j] = y1[j];
-      ss = ss1;
-      prior = pr1;
-      nacc += 1;
-    }
-    TCI_PHASE(4)
     // ---- stage 2 (k_accept2)
     bool acc2 = false;
+    double pr2 = 0.0;
     if (!acc && inb2) {
       nev += 1;
-      const double pr2 = prior_lds(y2, mu, sg, P, red);
+      pr2 = red[1];
       const double a32 = fmin(1.0, exp(-0.5 * (ss1 - ss2) / s2 - 0.5 * (pr1 - pr2)));
       const double l2 = exp(-0.5 * (ss2 - ss) / s2 - 0.5 * (pr2 - prior));
-      for (int j = t; j < P; j += kThreads) {
-        d1[j] = y2[j] - y1[j];
-        d0[j] = th[j] - y1[j];
-      }
-      __syncthreads();
-      tri_vecmat<2>(d1, d0, iRm, ld, P, part, z, y, L);
-      double q21 = 0.0, q01 = 0.0;
-      for (int j = t; j < P; j += kThreads) {
-        q21 += z[j] * z[j];
-        q01 += y[j] * y[j];
-      }
-      q21 = block_sum(q21, red);
-      q01 = block_sum(q01, red);
-      const double q1 = exp(-0.5 * (q21 - q01));
+      const double q1 = exp(-0.5 * (red[2] - red[3]));
       const double a13 = l2 * q1 * (1.0 - a32) / (1.0 - a12);
       acc2 = uniform_at(p.seed, c, step, P_U2) < a13;
-      if (acc2) {
-        for (int j = t; j < P; j += kThreads) th[j] = y2[j];
-        ss = ss2;
-        prior = pr2;
-        nacc += 1;
-      }
     }
-    TCI_PHASE(5)
-    if (!(acc || acc2)) nrej += 1;
-    if (p.updatesigma) s2 = 1.0 / gamma_at(p.seed, c, step, half_nobs, 2.0 / ss);
-    __syncthreads();
-    TCI_PHASE(6)
-    record_row(st, p, c, step, P, th, s2);
-    __syncthreads();
-    TCI_PHASE(7)
+    __syncthreads();  // red[] and th are rewritten below / next step
+    if (acc || acc2) {
+      const double* yy = acc ? y1 : y2;
+      for (int j = t; j < P; j += kThreads) th[j] = yy[j];
+      ss = acc ? ss1 : ss2;
+      prior = acc ? pr1 : pr2;
+      nacc += 1;
+    } else {
+      nrej += 1;
+    }
+    TCI_PHASE(4)
+  }
+  // the last row of the chunk: sigma2 draw and record
+  if (p.updatesigma) s2 = 1.0 / gamma_at(p.seed, c, s_end, half_nobs, 2.0 / ss);
+  __syncthreads();
+  record_vec(st, p, c, s_end, P, th, smn, sm2, t, kThreads);
+  if (w == 3 && lane == 0) record_s2(st, p, c, s_end, s2, s2a);
+  __syncthreads();
+  for (int j = t; j < P; j += kThreads) {
+    st.smean[c * ld + j] = smn[j];
+    st.sm2[c * ld + j] = sm2[j];
+  }
+  if (w == 3 && lane == 0) {
+    st.s2sum[c] = s2a.sum;
+    st.sq_mean[c] = s2a.qmean;
+    st.sq_m2[c] = s2a.qm2;
   }
 #undef TCI_PHASE
   if (TCI_CHAIN_PROFILE && t == 0 && st.prof != nullptr)
@@ -745,7 +851,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    hipStream_t stream) {
-  const size_t lds = (size_t)chain_lds_doubles(st.ld) * sizeof(double);
+  const size_t lds = (size_t)chain_lds_bytes(st.ld);
   if (lds > 48 * 1024 &&
       hipFuncSetAttribute((const void*)k_chain<RPL, NSEG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
           hipSuccess)
@@ -771,7 +877,7 @@ int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, 
 // two workgroups per CU). Thread t owns the packed upper-triangle entries e = t + 256 k of cov:
 // covupd runs on them in registers (no index arithmetic, one barrier pair per window row), then
 // an LDL'-form right-looking Cholesky on the packed triangle (one barrier per pivot; R rows are
-// scaled by 1/sqrt(pivot) at the end) and the row-by-row triangular inverse.
+// scaled by 1/sqrt(pivot) at the end).
 template <int KMAX>
 __global__ __launch_bounds__(kThreads) void k_adapt_packed(DramState st, DramParams p) {
   extern __shared__ __attribute__((aligned(16))) double dyn[];
@@ -786,11 +892,9 @@ __global__ __launch_bounds__(kThreads) void k_adapt_packed(DramState st, DramPar
   double* A = dyn;       // packed upper triangle, row i at off(i) = i*P - i*(i-1)/2
   double* dm = A + T;    // P
   double* dsq = dm + P;  // P
-  double* xs = dsq + P;  // P
   double* cvg = st.cov + c * ld * ld;
   double* mu = st.cmean + c * ld;
   double* R = st.R + c * ld * ld;
-  double* iR = st.iR + c * ld * ld;
   auto off = [P](int i) { return i * P - (i * (i - 1)) / 2; };
   // ---- the owned entries (i, j), walking the packed order from e = t in strides of 256
   int own[KMAX];
@@ -858,8 +962,7 @@ __global__ __launch_bounds__(kThreads) void k_adapt_packed(DramState st, DramPar
     if (s != 1.0) {
       for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
         const int i = (int)(e / P), j = (int)(e % P);
-        R[(int64_t)i * ld + j] *= s;
-        iR[(int64_t)i * ld + j] /= s;
+        R[(int64_t)i * ld + j] = f32_round(R[(int64_t)i * ld + j] * s);
       }
     }
     __syncthreads();
@@ -898,35 +1001,12 @@ __global__ __launch_bounds__(kThreads) void k_adapt_packed(DramState st, DramPar
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
     for (int i = t; i < P; i += kThreads) dsq[i] = sqrt(A[off(i)]);
     __syncthreads();
-    // C = D^-1/2 U (upper, C'C = cov + qcovadj*I); R = C * adascale
+    // C = D^-1/2 U (upper, C'C = cov + qcovadj*I); R = C * adascale, float-representable
 #pragma unroll
     for (int q = 0; q < KMAX; ++q) {
       if (own[q] >= 0) {
         const int i = own[q] >> 16, j = own[q] & 0xFFFF;
-        const double cij = A[t + kThreads * q] / dsq[i];
-        A[t + kThreads * q] = cij;
-        R[(int64_t)i * ld + j] = cij * sc;
-      }
-    }
-    __syncthreads();
-    // iR = C^-1 / adascale, in place, row by row from the bottom:
-    // X(i,j) = (d_ij - sum_{k=i+1..j} C(i,k) X(k,j)) / C(i,i)
-    for (int i = P - 1; i >= 0; --i) {
-      const int oi = off(i);
-      for (int k = i + t; k < P; k += kThreads) xs[k] = A[oi + k - i];
-      __syncthreads();
-      for (int j = i + t; j < P; j += kThreads) {
-        double s = (i == j) ? 1.0 : 0.0;
-        for (int k = i + 1; k <= j; ++k) s -= xs[k] * A[off(k) + j - k];
-        A[oi + j - i] = s / xs[i];
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int q = 0; q < KMAX; ++q) {
-      if (own[q] >= 0) {
-        const int i = own[q] >> 16, j = own[q] & 0xFFFF;
-        iR[(int64_t)i * ld + j] = A[t + kThreads * q] / sc;
+        R[(int64_t)i * ld + j] = f32_round(A[t + kThreads * q] / dsq[i] * sc);
       }
     }
   }
@@ -936,10 +1016,19 @@ __global__ __launch_bounds__(kThreads) void k_adapt_packed(DramState st, DramPar
 
 // Packed-adaptation bound: KMAX entries per thread and the LDS triangle + 3 vectors.
 constexpr int kAdaptKmax = 40;
-__host__ __device__ inline int64_t adapt_packed_lds_bytes(int64_t P) { return (P * (P + 1) / 2 + 3 * P) * 8; }
+__host__ __device__ inline int64_t adapt_packed_lds_bytes(int64_t P) { return (P * (P + 1) / 2 + 2 * P) * 8; }
 
 inline int finish() { return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP; }
 inline dim3 chain_grid(int64_t n) { return dim3((unsigned)n); }
+
+int launch_stage(void (*k)(DramState, DramParams), const DramState& st, const DramParams& p, void* stream) {
+  const size_t lds = (size_t)stage_lds_bytes(st.ld);
+  if (lds > 48 * 1024 &&
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return TCI_EHIP;
+  hipLaunchKernelGGL(k, chain_grid(st.n_chains), dim3(kThreads), lds, (hipStream_t)stream, st, p);
+  return finish();
+}
 
 }  // namespace
 
@@ -952,16 +1041,13 @@ int dram_launch_init_stats(const DramState& st, const DramParams& p, void* strea
   return finish();
 }
 int dram_launch_propose1(const DramState& st, const DramParams& p, void* stream) {
-  hipLaunchKernelGGL(k_propose1, chain_grid(st.n_chains), dim3(kThreads), 0, (hipStream_t)stream, st, p);
-  return finish();
+  return launch_stage(k_propose1, st, p, stream);
 }
 int dram_launch_accept1(const DramState& st, const DramParams& p, void* stream) {
-  hipLaunchKernelGGL(k_accept1, chain_grid(st.n_chains), dim3(kThreads), 0, (hipStream_t)stream, st, p);
-  return finish();
+  return launch_stage(k_accept1, st, p, stream);
 }
 int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream) {
-  hipLaunchKernelGGL(k_accept2, chain_grid(st.n_chains), dim3(kThreads), 0, (hipStream_t)stream, st, p);
-  return finish();
+  return launch_stage(k_accept2, st, p, stream);
 }
 int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
   if (p.pmax * (p.pmax + 1) / 2 <= (int64_t)kAdaptKmax * kThreads && adapt_packed_lds_bytes(p.pmax) <= 78 * 1024) {
@@ -993,7 +1079,7 @@ int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& k
   }
 }
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl) {
-  return chain_lds_doubles(ld) * 8 + 2 * (4 * 64 * rpl + 4 * rpl) * 8 + 64;
+  return chain_lds_bytes(ld) + 2 * (4 * 64 * rpl + 4 * rpl) * 8 + 64;
 }
 int dram_launch_step_incr(const DramState& st, void* stream) {
   hipLaunchKernelGGL(k_step_incr, dim3(1), dim3(64), 0, (hipStream_t)stream, st.step);

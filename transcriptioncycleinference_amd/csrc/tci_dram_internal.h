@@ -24,8 +24,7 @@ struct DramState {
   double* ss;              // SS of the current state
   double* prior;           // prior SS of the current state
   double* sigma2;          // error variance (model.sigma2, :259)
-  double* R;               // proposal Cholesky factor (upper): proposal = theta + z * R
-  double* iR;              // R^-1 (upper), for the delayed-rejection proposal ratio
+  double* R;               // proposal Cholesky factor (upper, float-representable): proposal = theta + z * R
   double* cov;             // running chain covariance / mean / weight (mcmcstat covupd)
   double* cmean;
   double* wsum;

@@ -80,13 +80,12 @@ class DramResult:
     s2chain: Optional[np.ndarray]
     elapsed_ms: float
     qcov_R: Optional[np.ndarray] = None   # final proposal factor (upper, R'R = mcmcstat results.qcov)
-    qcov_iR: Optional[np.ndarray] = None  # its inverse
 
 
 def dram_run(lk, cell_id, theta0, lower, upper, prior_mu, prior_sig, qcov_diag, sigma2_0,
              opts: DramOptions, want_qcov: bool = False) -> DramResult:
     """Run one chain per row on the device (``tci_dram_run``). Arrays are (n_chains, ld).
-    ``want_qcov``: also return the final proposal factor R and its inverse (n_chains, ld, ld)."""
+    ``want_qcov``: also return the final proposal factor R (n_chains, ld, ld)."""
     f = lambda a: np.ascontiguousarray(a, np.float64)  # noqa: E731
     theta0, lower, upper, prior_mu, prior_sig, qcov_diag = map(f, (theta0, lower, upper, prior_mu, prior_sig,
                                                                     qcov_diag))
@@ -100,16 +99,15 @@ def dram_run(lk, cell_id, theta0, lower, upper, prior_mu, prior_sig, qcov_diag, 
     chain = np.empty((n_keep, n, ld)) if n_keep else None
     s2c = np.empty((n_keep, n)) if n_keep else None
     qR = np.empty((n, ld, ld)) if want_qcov else None
-    qiR = np.empty((n, ld, ld)) if want_qcov else None
     out = _lib.tci_dram_outputs(_lib.ptr(mean, _lib._dp), _lib.ptr(std, _lib._dp), _lib.ptr(fin, _lib._dp),
                                 _lib.ptr(smean, _lib._dp), _lib.ptr(sstd, _lib._dp), _lib.ptr(acc, _lib._dp),
                                 _lib.ptr(nev, _lib._i64p), _lib.ptr(chain, _lib._dp), _lib.ptr(s2c, _lib._dp),
-                                _lib.ptr(qR, _lib._dp), _lib.ptr(qiR, _lib._dp), 0.0)
+                                _lib.ptr(qR, _lib._dp), 0.0)
     o = opts.to_c()
     P = lambda a: _lib.ptr(a, _lib._dp)  # noqa: E731
     lk._check(lk._lib.tci_dram_run(lk._h, C.byref(o), n, _lib.ptr(cid, _lib._i32p), P(theta0), P(lower), P(upper),
                                    P(prior_mu), P(prior_sig), P(qcov_diag), P(s20), ld, C.byref(out)))
-    return DramResult(mean, std, fin, smean, sstd, acc, nev, chain, s2c, float(out.elapsed_ms), qR, qiR)
+    return DramResult(mean, std, fin, smean, sstd, acc, nev, chain, s2c, float(out.elapsed_ms), qR)
 
 
 # ---------------------------------------------------------------------------
