@@ -873,86 +873,155 @@ int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, 
 }
 
 
-// Adaptation for chains whose packed covariance fits in LDS (P(P+1)/2 doubles; P <= 139 keeps
-// two workgroups per CU). Thread t owns the packed upper-triangle entries e = t + 256 k of cov:
-// covupd runs on them in registers (no index arithmetic, one barrier pair per window row), then
-// an LDL'-form right-looking Cholesky on the packed triangle (one barrier per pivot; R rows are
-// scaled by 1/sqrt(pivot) at the end).
-template <int KMAX>
-__global__ __launch_bounds__(kThreads) void k_adapt_packed(DramState st, DramParams p) {
+// Adaptation for chains whose packed covariance fits in LDS (P(P+1)/2 doubles: P <= 139 keeps two
+// workgroups per CU). Thread t owns the 4x4 tiles t, t + 256, .. (row-major over the upper
+// triangle of the tile grid) in registers.
+//   covupd: the window's rows (staged through LDS in batches) give the batch mean and scatter
+//     sum_r (x_r - m)'(x_r - m) (16 FMAs per tile and row), merged into (cov, mean, wsum) by the
+//     pairwise-update formula -- the same numbers as mcmcstat's row-by-row recurrence in exact
+//     arithmetic, with 2 barriers per batch instead of 2 per row.
+//   Cholesky of cov + qcovadj I: blocked LDL' with 4-column panels: a tile row is stored to the
+//     packed LDS triangle when it becomes the panel, wave 0 eliminates inside the panel, every
+//     owner applies the rank-4 update to its later tiles in registers (2 barriers per panel).
+//     R rows are the panel rows scaled by adascale / sqrt(pivot).
+constexpr int kAdaptTiles = 3;  // tiles per thread: NT(NT+1)/2 <= 768, NT = ceil(P/4)
+__host__ __device__ inline int adapt_ls(int P) { return (P + 3) & ~3; }
+__host__ __device__ inline int64_t adapt_tiles_lds_bytes(int64_t P) {
+  const int64_t tri = P * (P + 1) / 2, Ls = (P + 3) & ~3;
+  return (tri + 2 * Ls + 8) * 8;
+}
+
+__global__ __launch_bounds__(kThreads) void k_adapt_tiles(DramState st, DramParams p) {
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int fail;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int64_t c = blockIdx.x;
   const int64_t step = *st.step;
   if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
   const int64_t ld = st.ld;
   const int P = st.npar[c];
-  const int T = P * (P + 1) / 2;
-  double* A = dyn;       // packed upper triangle, row i at off(i) = i*P - i*(i-1)/2
-  double* dm = A + T;    // P
-  double* dsq = dm + P;  // P
+  const int NT = (P + 3) >> 2, Ls = adapt_ls(P);
+  const int tri = P * (P + 1) / 2;
+  double* A = dyn;         // phase 1-2: window batches [rb][Ls]; phase 4: packed upper triangle
+  double* mb = A + tri;    // batch mean (Ls)
+  double* mo = mb + Ls;    // old mean (Ls)
   double* cvg = st.cov + c * ld * ld;
   double* mu = st.cmean + c * ld;
   double* R = st.R + c * ld * ld;
   auto off = [P](int i) { return i * P - (i * (i - 1)) / 2; };
-  // ---- the owned entries (i, j), walking the packed order from e = t in strides of 256
-  int own[KMAX];
-  double a[KMAX];
+  // ---- owned tiles (ti, tj), ti <= tj, by walking the row-major tile order from t
+  int ti_[kAdaptTiles], tj_[kAdaptTiles];
   {
-    int i = 0, j = t;
-    while (i < P && j >= P) {
-      j = j - P + i + 1;
-      ++i;
+    int ti = 0, tj = t;
+    while (ti < NT && tj >= NT) {
+      tj = tj - NT + ti + 1;
+      ++ti;
     }
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const bool v = i < P;
-      own[k] = v ? (i << 16) | j : -1;
-      a[k] = v ? cvg[(int64_t)i * ld + j] : 0.0;
-      j += kThreads;
-      while (i < P && j >= P) {
-        j = j - P + i + 1;
-        ++i;
+    for (int k = 0; k < kAdaptTiles; ++k) {
+      ti_[k] = ti < NT ? ti : -1;
+      tj_[k] = tj;
+      tj += kThreads;
+      while (ti < NT && tj >= NT) {
+        tj = tj - NT + ti + 1;
+        ++ti;
       }
     }
   }
-  // ---- covupd over the window rows (chain rows step-adaptint+1 .. step), mcmcstat's recurrence
-  double ws = st.wsum[c];
-  double mu0 = t < P ? mu[t] : 0.0, mu1 = t + kThreads < P ? mu[t + kThreads] : 0.0;
-  for (int64_t r = 0; r < p.adaptint; ++r) {
-    const double* x = st.window + (c * p.adaptint + r) * ld;
-    if (ws == 0.0) {  // first row: mean = x, cov = 0
-      if (t < P) mu0 = x[t];
-      if (t + kThreads < P) mu1 = x[t + kThreads];
-      ws = 1.0;
-      continue;
+  const int nb = (int)p.adaptint;
+  const int rb = max(1, min(nb, tri / Ls));  // rows per LDS batch
+  const double* win = st.window + c * p.adaptint * ld;
+  // ---- pass 1: batch mean (row order fixed: deterministic)
+  double s0 = 0.0, s1 = 0.0;
+  for (int r0 = 0; r0 < nb; r0 += rb) {
+    const int n = min(rb, nb - r0);
+    for (int e = t; e < n * Ls; e += kThreads) {
+      const int r = e / Ls, j = e - r * Ls;
+      A[e] = j < P ? win[(int64_t)(r0 + r) * ld + j] : 0.0;
     }
-    const double d0 = t < P ? x[t] - mu0 : 0.0, d1 = t + kThreads < P ? x[t + kThreads] - mu1 : 0.0;
-    if (t < P) dm[t] = d0;
-    if (t + kThreads < P) dm[t + kThreads] = d1;
     __syncthreads();
-    // xcov = oldcov + w/(w+oldwsum-1) * (oldwsum/(w+oldwsum) * d'd - oldcov), w = 1
-    const double f1 = 1.0 / ws, f2 = ws / (ws + 1.0);
+    for (int r = 0; r < n; ++r) {
+      if (t < Ls) s0 += A[r * Ls + t];
+      if (t + kThreads < Ls) s1 += A[r * Ls + t + kThreads];
+    }
+    __syncthreads();
+  }
+  if (t < Ls) {
+    mb[t] = t < P ? s0 / (double)nb : 0.0;
+    mo[t] = t < P ? mu[t] : 0.0;
+  }
+  if (t + kThreads < Ls) {
+    mb[t + kThreads] = t + kThreads < P ? s1 / (double)nb : 0.0;
+    mo[t + kThreads] = t + kThreads < P ? mu[t + kThreads] : 0.0;
+  }
+  __syncthreads();
+  // ---- pass 2: scatter of the deviations from the batch mean, per owned tile
+  double acc[kAdaptTiles][16];
+  double mi[kAdaptTiles][4], mj[kAdaptTiles][4];
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      if (own[k] >= 0) {
-        const int i = own[k] >> 16, j = own[k] & 0xFFFF;
-        a[k] = a[k] + f1 * (f2 * dm[i] * dm[j] - a[k]);
+  for (int k = 0; k < kAdaptTiles; ++k) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[k][q] = 0.0;
+    const int ti = max(ti_[k], 0), tj = ti_[k] >= 0 ? tj_[k] : 0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      mi[k][a] = mb[4 * ti + a];
+      mj[k][a] = mb[4 * tj + a];
+    }
+  }
+  for (int r0 = 0; r0 < nb; r0 += rb) {
+    const int n = min(rb, nb - r0);
+    for (int e = t; e < n * Ls; e += kThreads) {
+      const int r = e / Ls, j = e - r * Ls;
+      A[e] = j < P ? win[(int64_t)(r0 + r) * ld + j] : 0.0;
+    }
+    __syncthreads();
+    for (int r = 0; r < n; ++r) {
+      const double* x = A + r * Ls;
+#pragma unroll
+      for (int k = 0; k < kAdaptTiles; ++k) {
+        if (ti_[k] < 0) continue;
+        const double2* xi = reinterpret_cast<const double2*>(x + 4 * ti_[k]);
+        const double2* xj = reinterpret_cast<const double2*>(x + 4 * tj_[k]);
+        const double2 i01 = xi[0], i23 = xi[1], j01 = xj[0], j23 = xj[1];
+        const double di[4] = {i01.x - mi[k][0], i01.y - mi[k][1], i23.x - mi[k][2], i23.y - mi[k][3]};
+        const double dj[4] = {j01.x - mj[k][0], j01.y - mj[k][1], j23.x - mj[k][2], j23.y - mj[k][3]};
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[k][4 * a + b] = fma(di[a], dj[b], acc[k][4 * a + b]);
       }
     }
-    mu0 = mu0 + d0 / (ws + 1.0);
-    mu1 = mu1 + d1 / (ws + 1.0);
-    ws += 1.0;
-    __syncthreads();  // dm is rewritten by the next row
+    __syncthreads();
   }
+  // ---- merge (cov, mean, wsum) with the batch: n = na + nb, d = m_batch - m_old
+  const double na = st.wsum[c], n = na + (double)nb;
+  const double fcross = na * (double)nb / n;
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    if (own[k] >= 0) cvg[(int64_t)(own[k] >> 16) * ld + (own[k] & 0xFFFF)] = a[k];
+  for (int k = 0; k < kAdaptTiles; ++k) {
+    if (ti_[k] < 0) continue;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int i = 4 * ti_[k] + a, j = 4 * tj_[k] + b;
+        if (i >= P || j >= P || j < i) continue;
+        double cv;
+        if (n <= 1.0) {
+          cv = 0.0;  // a single row so far: covariance 0 (the recurrence's first row)
+        } else if (na == 0.0) {
+          cv = acc[k][4 * a + b] / (n - 1.0);
+        } else {
+          const double di = mb[i] - mo[i], dj = mb[j] - mo[j];
+          cv = (cvg[(int64_t)i * ld + j] * (na - 1.0) + acc[k][4 * a + b] + di * dj * fcross) / (n - 1.0);
+        }
+        cvg[(int64_t)i * ld + j] = cv;
+        acc[k][4 * a + b] = cv + (i == j ? p.qcovadj : 0.0);  // the matrix the Cholesky factors
+      }
   }
-  if (t < P) mu[t] = mu0;
-  if (t + kThreads < P) mu[t + kThreads] = mu1;
-  if (t == 0) st.wsum[c] = ws;
+  for (int j = t; j < P; j += kThreads) mu[j] = na == 0.0 ? mb[j] : mo[j] + (mb[j] - mo[j]) * ((double)nb / n);
+  if (t == 0) st.wsum[c] = n;
   if (step < p.burnintime) {
     // burn-in: no covariance adaptation, only scaling by the window's rejection rate
     const double rate = (double)st.nrej_win[c] / (double)p.adaptint;
@@ -969,54 +1038,73 @@ __global__ __launch_bounds__(kThreads) void k_adapt_packed(DramState st, DramPar
     if (t == 0) st.nrej_win[c] = 0;
     return;
   }
-  // ---- Cholesky of cov + qcovadj*I: eliminate with unscaled pivot rows, A = U' D^-1 U
-#pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    if (own[k] >= 0) {
-      const int i = own[k] >> 16, j = own[k] & 0xFFFF;
-      A[t + kThreads * k] = a[k] + (i == j ? p.qcovadj : 0.0);
-    }
-  }
+  // ---- blocked LDL' of cov + qcovadj I on the packed triangle
   if (t == 0) fail = 0;
   __syncthreads();
-  for (int k = 0; k < P; ++k) {
-    const int ok = off(k);
-    const double d = A[ok];
-    if (!(d > 0.0) || !isfinite(d)) {  // uniform: every thread reads the same pivot
-      if (t == 0) fail = 1;
-      break;
-    }
-    const double inv = 1.0 / d;
+  for (int pp = 0; pp < NT; ++pp) {
 #pragma unroll
-    for (int q = 0; q < KMAX; ++q) {
-      if (own[q] >= 0) {
-        const int i = own[q] >> 16, j = own[q] & 0xFFFF;
-        if (i > k) A[t + kThreads * q] -= A[ok + i - k] * A[ok + j - k] * inv;
+    for (int k = 0; k < kAdaptTiles; ++k) {
+      if (ti_[k] != pp) continue;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int i = 4 * pp + a, j = 4 * tj_[k] + b;
+          if (i < P && j < P && j >= i) A[off(i) + j - i] = acc[k][4 * a + b];
+        }
+    }
+    __syncthreads();
+    const int k0 = 4 * pp, k1 = min(4 * pp + 3, P - 1);
+    if (w == 0) {  // eliminate inside the panel rows
+      for (int k = k0; k <= k1; ++k) {
+        const int ok = off(k);
+        const double d = A[ok];
+        if (!(d > 0.0) || !isfinite(d)) {
+          if (lane == 0) fail = 1;
+          break;
+        }
+        for (int kp = k + 1; kp <= k1; ++kp) {
+          const double f = A[ok + kp - k] / d;
+          const int okp = off(kp);
+          for (int j = kp + lane; j < P; j += 64) A[okp + j - kp] -= f * A[ok + j - k];
+        }
+        wave_sync();
       }
     }
     __syncthreads();
+    if (fail) break;
+    // rank-4 update of every owned later tile: A[i][j] -= A[k][i] * A[k][j] / A[k][k]
+#pragma unroll
+    for (int k = 0; k < kAdaptTiles; ++k) {
+      if (ti_[k] <= pp) continue;
+      for (int kk = k0; kk <= k1; ++kk) {
+        const int ok = off(kk);
+        const double inv = 1.0 / A[ok];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int i = 4 * ti_[k] + a;
+          const double sa = (i < P ? A[ok + i - kk] : 0.0) * inv;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int j = 4 * tj_[k] + b;
+            acc[k][4 * a + b] -= sa * (j < P ? A[ok + j - kk] : 0.0);
+          }
+        }
+      }
+    }
   }
   __syncthreads();
   if (!fail) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
-    for (int i = t; i < P; i += kThreads) dsq[i] = sqrt(A[off(i)]);
-    __syncthreads();
-    // C = D^-1/2 U (upper, C'C = cov + qcovadj*I); R = C * adascale, float-representable
-#pragma unroll
-    for (int q = 0; q < KMAX; ++q) {
-      if (own[q] >= 0) {
-        const int i = own[q] >> 16, j = own[q] & 0xFFFF;
-        R[(int64_t)i * ld + j] = f32_round(A[t + kThreads * q] / dsq[i] * sc);
-      }
+    for (int i = 0; i < P; ++i) {
+      const int oi = off(i);
+      const double di = sqrt(A[oi]);
+      for (int j = i + t; j < P; j += kThreads) R[(int64_t)i * ld + j] = f32_round(A[oi + j - i] / di * sc);
     }
   }
   __syncthreads();
   if (t == 0) st.nrej_win[c] = 0;
 }
-
-// Packed-adaptation bound: KMAX entries per thread and the LDS triangle + 3 vectors.
-constexpr int kAdaptKmax = 40;
-__host__ __device__ inline int64_t adapt_packed_lds_bytes(int64_t P) { return (P * (P + 1) / 2 + 2 * P) * 8; }
 
 inline int finish() { return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP; }
 inline dim3 chain_grid(int64_t n) { return dim3((unsigned)n); }
@@ -1050,14 +1138,13 @@ int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream) 
   return launch_stage(k_accept2, st, p, stream);
 }
 int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
-  if (p.pmax * (p.pmax + 1) / 2 <= (int64_t)kAdaptKmax * kThreads && adapt_packed_lds_bytes(p.pmax) <= 78 * 1024) {
-    const size_t bytes = (size_t)adapt_packed_lds_bytes(p.pmax);
-    if (bytes > 48 * 1024 &&
-        hipFuncSetAttribute((const void*)k_adapt_packed<kAdaptKmax>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)bytes) != hipSuccess)
+  const int64_t ntile = (p.pmax + 3) / 4;
+  if (ntile * (ntile + 1) / 2 <= (int64_t)kAdaptTiles * kThreads && adapt_tiles_lds_bytes(p.pmax) <= 78 * 1024) {
+    const size_t bytes = (size_t)adapt_tiles_lds_bytes(p.pmax);
+    if (bytes > 48 * 1024 && hipFuncSetAttribute((const void*)k_adapt_tiles, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)bytes) != hipSuccess)
       return TCI_EHIP;
-    hipLaunchKernelGGL(k_adapt_packed<kAdaptKmax>, chain_grid(st.n_chains), dim3(kThreads), bytes,
-                       (hipStream_t)stream, st, p);
+    hipLaunchKernelGGL(k_adapt_tiles, chain_grid(st.n_chains), dim3(kThreads), bytes, (hipStream_t)stream, st, p);
     return finish();
   }
   const size_t lds = p.lds_matrix ? (size_t)p.lds_matrix : 0;
