@@ -30,6 +30,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+SIMDS = 256 * 4        # 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9       # max engine clock (MI355X_MICROARCH.md)
 CONSTRUCT = "P2P-MS2v5-LacZ-PP7v4"
 
 
@@ -75,17 +77,32 @@ def algorithmic_bytes(cells, cid, active) -> int:
     return int(per_active + 9 * len(cid) + 24 * lens.sum())
 
 
-def load_traffic(workload: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
+def load_pmc(workload: str) -> dict:
+    """The committed rocprofv3 PMC summary of this workload's kernel (profiles/pmc_traffic.json,
+    written by scripts/pmc_summary.py), or {} when there is none."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
         if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
+            return d
     except (OSError, ValueError):
         pass
-    return None
+    return {}
+
+
+def valu_issue(pmc: dict, kernel_ms: float):
+    """The bound that actually limits this FP64 kernel: VALU issue. A wave64 VALU instruction
+    occupies its SIMD (16 lanes) for 4 cycles; FP64 FMA runs at that full rate on gfx950
+    (78.6 TF/s = 1024 SIMDs x 16 lanes x 2 x 2.4 GHz). Peak = 1024 x 2.4e9 / 4 wave-instructions/s.
+    achieved = SQ_INSTS_VALU per launch (committed PMC pass) / the live per-launch kernel time."""
+    insts = (pmc.get("counters_mean_per_launch") or {}).get("SQ_INSTS_VALU")
+    if not insts or kernel_ms <= 0:
+        return None
+    peak = SIMDS * CLOCK_HZ / 4.0
+    achieved = insts / (kernel_ms * 1e-3)
+    return {"achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "G VALU wave-instr/s", "frac": achieved / peak,
+            "valu_insts_per_launch": insts, "source": pmc.get("source")}
 
 
 def cpu_baseline(cells, theta, cid, active, seconds: float):
@@ -117,19 +134,25 @@ def cpu_baseline(cells, theta, cid, active, seconds: float):
                       f"OpenMP {threads} threads"}
 
 
-def end_to_end(lk, n_steps: int):
+def end_to_end(lk, n_steps: int, seed: int, reduce=None):
     """SURVEY §8(d) mode (ii): the reference's whole fit -- one DRAM chain per TestData cell,
-    n_steps (200k) steps, n_burn = n_steps/20, GPU-resident sampler; every ssfun call is the
-    batched kernel. Reported beside `value` (a step there is one batched launch)."""
+    n_steps (200k) steps, n_burn = n_steps/20, GPU-resident sampler (every ssfun evaluation runs
+    inside the fused chain kernel). Reported beside `value` (a step there is one batched launch).
+    With N ranks every rank fits its own replica (weak scaling, like `value`); `reduce(x, op)`
+    combines over ranks: evals are summed, the wall time is the max."""
     from transcriptioncycleinference_amd.mcmc import fit
 
     t0 = time.perf_counter()
-    fr = fit(lk, n_steps=n_steps, n_burn=max(1, n_steps // 20), seed=1)
+    fr = fit(lk, n_steps=n_steps, n_burn=max(1, n_steps // 20), seed=seed)
     wall = time.perf_counter() - t0
-    return {"n_steps": n_steps, "chains": len(fr.MCMCresults), "device_s": fr.elapsed_ms * 1e-3, "wall_s": wall,
-            "ssfun_evals": fr.n_evals, "value": fr.n_evals / (fr.elapsed_ms * 1e-3), "unit": "SS evals/s",
-            "us_per_step": fr.elapsed_ms * 1e3 / max(n_steps - 1, 1),
-            "accept_rate_median": float(np.median(fr.accept_rate))}
+    dev_s, evals, chains = fr.elapsed_ms * 1e-3, int(fr.n_evals), len(fr.MCMCresults)
+    if reduce is not None:
+        dev_s, wall = reduce(dev_s, "max"), reduce(wall, "max")
+        evals, chains = int(reduce(evals, "sum")), int(reduce(chains, "sum"))
+    return {"n_steps": n_steps, "chains": chains, "device_s": dev_s, "wall_s": wall,
+            "ssfun_evals": evals, "value": evals / dev_s, "unit": "SS evals/s",
+            "us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
+            "accept_rate_median_rank0": float(np.median(fr.accept_rate))}
 
 
 def main():
@@ -222,7 +245,8 @@ def main():
     workload = f"TestData-299cells-x{args.proposals}proposals"
     alg = algorithmic_bytes(cells, cid, active)
     achieved = alg / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(workload)
+    pmc = load_pmc(workload)
+    traffic = pmc.get("hbm_bytes_per_launch")
     res = {
         "metric": "forward-model SS evals/sec, 299-cell TestData, 200k-step chains @1/2/4/8 GPU",
         "value": total_active * args.steps / elapsed,
@@ -255,7 +279,8 @@ def main():
             "traffic": traffic,
             "kernel_ms": kernel_ms,
             "algorithmic_bytes_per_launch": alg,
-            "note": "FP64-VALU/latency-bound path; HBM fraction reported as the north star asks (DESIGN.md)",
+            "note": "FP64-VALU-issue-bound path (see 'valu'); HBM fraction reported as the north star asks (DESIGN.md §3)",
+            "valu": valu_issue(pmc, kernel_ms),
         },
         "results_finite": finite_ok,
     }
@@ -270,8 +295,17 @@ def main():
         res["host_api_pcie_inclusive"] = {"value": n_active / h_el, "unit": "SS evals/s",
                                           "ms_per_call": h_el * 1e3, "bytes_h2d": int(theta.nbytes + cid.nbytes
                                                                                     + active.nbytes)}
-    if rank == 0 and world == 1 and args.dram_steps > 1:
-        res["end_to_end_dram"] = end_to_end(lk, args.dram_steps)
+    if args.dram_steps > 1:
+        def reduce(x, op):
+            if not distributed:
+                return x
+            t = torch.tensor([float(x)], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+            return float(t.item())
+
+        if distributed:
+            dist.barrier()
+        res["end_to_end_dram"] = end_to_end(lk, args.dram_steps, seed=1 + rank, reduce=reduce)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cells, theta, cid, active, args.cpu_seconds)
     if rank == 0:

@@ -149,14 +149,20 @@ typedef struct {
   uint64_t seed;
   int32_t engine;       /* TCI_DRAM_AUTO / TCI_DRAM_FUSED / TCI_DRAM_BATCHED (below) */
   int32_t reserved;
+  const int64_t* chain_keys; /* optional [n_chains]: chain c draws from RNG stream chain_keys[c]
+                                (NULL: stream c). Keying chains by their global cell index makes a
+                                shard of a run (its cells on one GPU) reproduce the unsharded chains */
 } tci_dram_options;
 
 /* DRAM engines; both give identical chains for the same seed.
- *   FUSED:   one workgroup per chain runs a chunk of steps (up to the next adaptation) inside one
- *            kernel, with its ssfun evaluations in the loop: latency-bound runs (few chains).
+ *   FUSED:   per chunk of steps (up to the next adaptation) one wide launch draws every
+ *            state-independent random quantity (proposal offsets z*R on MFMA, uniforms, Gamma
+ *            variates), then one workgroup per chain walks the chunk with its ssfun evaluations in
+ *            the loop (one workgroup barrier per step): latency-bound runs (few chains).
  *   BATCHED: one launch per stage, every chain's ssfun in the batched likelihood kernel, replayed
  *            as a hipGraph per adaptation window: many chains, or cells too long for FUSED.
- *   AUTO:    FUSED when its workgroup fits twice in a CU (LDS) and there are at most 8 chains per CU. */
+ *   AUTO:    FUSED when its draws pass fits a CU's LDS (P <= ~225) and there are at most 8 chains
+ *            per CU. */
 #define TCI_DRAM_AUTO 0
 #define TCI_DRAM_FUSED 1
 #define TCI_DRAM_BATCHED 2

@@ -61,3 +61,67 @@ def test_gloo_world2_shard_and_gather():
     np.testing.assert_array_equal(full[:, 1], cells.lengths)
     assert bounds[0] == 0 and bounds[-1] == 299
     assert mx == max(bounds[1] - bounds[0], bounds[2] - bounds[1])
+
+
+def _pack_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from transcriptioncycleinference_amd import testdata
+    from transcriptioncycleinference_amd.parallel import cell_weights, gather_rows, pack_results, shard_bounds
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cells = testdata()
+    b = shard_bounds(cell_weights(cells.lengths), world)
+    fr = _fake_fit(cells, range(int(b[rank]), int(b[rank + 1])))
+    rows = gather_rows(pack_results(fr, int(cells.lengths.max())))
+    if rank == 0:
+        q.put(rows)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _fake_fit(cells, ids):
+    """A FitResult with deterministic per-cell values (stand-in for the GPU fit)."""
+    from transcriptioncycleinference_amd.mcmc import RESULT_FIELDS, FitResult
+
+    res, plots = [], []
+    for c in ids:
+        n = int(cells.lengths[c])
+        r = {f: float(c) + k / 100 for k, f in enumerate(RESULT_FIELDS)}
+        r["mean_dR"], r["sigma_dR"] = np.arange(n) + c, np.arange(n) * 0.5 - c
+        r["cell_index"], r["ApprovedFits"] = c + 1, c % 2
+        res.append(r)
+        plots.append({"simMS2": np.full(n, c * 1.5), "simPP7": np.full(n, -c * 1.0)})
+    return FitResult(cells.name, res, plots, [{} for _ in ids], np.array([c / 1000 for c in ids]), 0, 0.0)
+
+
+def test_gloo_world2_sharded_results_gather_round_trip():
+    """parallel.fit_sharded's data path on CPU: per-rank packed results, one all-gather, unpacked
+    into the whole dataset's MCMCresults/MCMCplot in cell order (the GPU fit itself is covered by
+    tests/test_dram_gpu.py::test_sharded_fit_world2_equals_the_one_gpu_fit)."""
+    from transcriptioncycleinference_amd import testdata
+    from transcriptioncycleinference_amd.parallel import unpack_results
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pack_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    rows = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cells = testdata()
+    fr = unpack_results(rows[::-1], cells, cells.name, 7, 1.0)  # any row order
+    want = _fake_fit(cells, range(299))
+    assert [r["cell_index"] for r in fr.MCMCresults] == list(range(1, 300))
+    for a, b, pa, pb in zip(fr.MCMCresults, want.MCMCresults, fr.MCMCplot, want.MCMCplot):
+        for f in a:
+            np.testing.assert_array_equal(a[f], b[f], err_msg=f)
+        np.testing.assert_array_equal(pa["simMS2"], pb["simMS2"])
+        np.testing.assert_array_equal(pa["simPP7"], pb["simPP7"])
+        assert len(pa["t_plot"]) == len(a["mean_dR"])
+    np.testing.assert_array_equal(fr.accept_rate, want.accept_rate)

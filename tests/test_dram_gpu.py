@@ -286,3 +286,77 @@ def test_adapted_proposal_is_the_scaled_chain_covariance(lk, engine):
         Q = R.T @ R
         want = (2.4 ** 2 / P) * C
         np.testing.assert_allclose(Q, want, rtol=1e-6, atol=1e-6 * np.abs(want).max())
+
+
+@pytest.mark.parametrize("engine", ["fused", "batched"])
+def test_chain_keys_let_a_shard_reproduce_the_full_run(lk, engine):
+    """chains keyed by their global index reproduce, on a shard (a subset of the
+    chains run alone, as one GPU of a sharded fit would), the rows of the unsharded run bitwise."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions, dram_run
+
+    ids = list(range(40, 100))
+    o = DramOptions(n_steps=450, burnintime=200, adaptint=100, stats_from=100, thin=9, seed=5, engine=engine)
+    x0, lo, hi, mu, sg, J0 = setup_rows(lk.cells, ids, 0)
+    keys = np.array(ids, np.int64)
+    full = dram_run(lk, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, chain_keys=keys)
+    for a, b in ((0, 25), (25, 60)):
+        sl = slice(a, b)
+        part = dram_run(lk, np.array(ids[sl], np.int32), x0[sl], lo[sl], hi[sl], mu[sl], sg[sl], J0[sl], 1.0, o,
+                        chain_keys=keys[sl])
+        for f in ("mean", "std", "final_theta", "sigma_mean", "accept_rate", "n_evals"):
+            np.testing.assert_array_equal(getattr(part, f), getattr(full, f)[sl], err_msg=f)
+        np.testing.assert_array_equal(part.chain, full.chain[:, sl])
+    # no keys = keyed by row index
+    d0 = dram_run(lk, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o)
+    d1 = dram_run(lk, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o,
+                  chain_keys=np.arange(len(ids), dtype=np.int64))
+    np.testing.assert_array_equal(d0.chain, d1.chain)
+
+
+def _sharded_worker(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+
+    from transcriptioncycleinference_amd import Likelihood, testdata
+    from transcriptioncycleinference_amd.parallel import fit_sharded, pack_results
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cells = testdata()
+    with Likelihood(cells, "P2P-MS2v5-LacZ-PP7v4", device=0) as L:
+        fr = fit_sharded(L, n_steps=400, n_burn=150, seed=4)
+    if rank == 0:
+        q.put(pack_results(fr, int(cells.lengths.max())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_fit_world2_equals_the_one_gpu_fit(lk):
+    """parallel.fit_sharded over 2 ranks (gloo, both on this GPU; RCCL on a multi-GPU node): each
+    rank fits its cell range, one all-gather assembles MCMCresults/MCMCplot -- equal bitwise to
+    fitting every cell in one process."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from transcriptioncycleinference_amd.mcmc import fit
+    from transcriptioncycleinference_amd.parallel import pack_results
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = pack_results(fit(lk, n_steps=400, n_burn=150, seed=4), int(lk.cells.lengths.max()))
+    assert got.shape == want.shape == (299, want.shape[1])
+    np.testing.assert_array_equal(got, want)

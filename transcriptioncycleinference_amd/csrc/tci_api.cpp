@@ -506,6 +506,7 @@ int tci_dram_defaults(tci_dram_options* o) {
   o->seed = 20201028;
   o->engine = TCI_DRAM_AUTO;
   o->reserved = 0;
+  o->chain_keys = nullptr;
   return TCI_OK;
 }
 
@@ -554,6 +555,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   int32_t *d_cell, *d_npar, *d_nobs;
   double *d_lower, *d_upper, *d_pmu, *d_psig, *d_qdiag, *d_s20;
   d_cell = A.alloc<int32_t>(n, &e);
+  int64_t* d_key = A.alloc<int64_t>(n, &e);
   d_npar = A.alloc<int32_t>(n, &e);
   d_nobs = A.alloc<int32_t>(n, &e);
   d_lower = A.alloc<double>(n * L, &e);
@@ -564,6 +566,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   d_s20 = A.alloc<double>(n, &e);
   if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dram inputs)");
   st.cell = d_cell;
+  st.key = d_key;
   st.npar = d_npar;
   st.nobs = d_nobs;
   st.lower = d_lower;
@@ -598,17 +601,18 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(sq_mean, double, n);
   TCI_ALLOC(sq_m2, double, n);
   TCI_ALLOC(step, int64_t, 1);
-#ifdef TCI_CHAIN_PROFILE
-  TCI_ALLOC(prof, int64_t, 8);
-  TCI_HIP(ctx, hipMemsetAsync(st.prof, 0, 8 * sizeof(int64_t), ctx->stream));
-#endif
   if (n_keep > 0 && (out->chain || out->s2chain)) {
     TCI_ALLOC(chain_out, double, (size_t)n_keep * n * L);
     TCI_ALLOC(s2_out, double, (size_t)n_keep * n);
+    // entries past a chain's P are never written: zero them so outputs are deterministic
+    TCI_HIP(ctx, hipMemsetAsync(st.chain_out, 0, (size_t)n_keep * n * L * sizeof(double), ctx->stream));
   }
 #undef TCI_ALLOC
   hipStream_t s = ctx->stream;
   TCI_HIP(ctx, hipMemcpyAsync(d_cell, cell_id, n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  std::vector<int64_t> keys(n);
+  for (size_t c = 0; c < n; ++c) keys[c] = opt->chain_keys ? opt->chain_keys[c] : (int64_t)c;
+  TCI_HIP(ctx, hipMemcpyAsync(d_key, keys.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, s));
   TCI_HIP(ctx, hipMemcpyAsync(d_npar, npar.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
   TCI_HIP(ctx, hipMemcpyAsync(d_nobs, nobs.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
   TCI_HIP(ctx, hipMemcpyAsync(d_lower, lower, n * L * sizeof(double), hipMemcpyHostToDevice, s));
@@ -651,21 +655,29 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   const int64_t ai = opt->adaptint;
   int n_cu = 0;
   TCI_HIP(ctx, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-  // the fused engine's workgroup keeps the chain's vectors, R (fp32) and two evaluation tables in
-  // LDS: it must fit a CU (160 KB); AUTO also wants two workgroups per CU (<= 80 KB)
+  // the fused engine's draws pass keeps a chain's R (packed fp32) and a tile of normals and products
+  // in LDS: it must fit a CU (160 KB). AUTO picks it for up to 8 chains per CU (the chain walk is
+  // latency-bound; beyond that the batched engine's wide launches keep more of the chip busy).
   const int64_t fused_lds = tci::dram_chain_lds_bytes(ld, ctx->rpl);
   const bool fused_fits = fused_lds <= 160 * 1024;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   bool fused = opt->engine == TCI_DRAM_FUSED;
   if (opt->engine == TCI_DRAM_AUTO)
-    fused = fused_lds <= 80 * 1024 && n_chains <= 8 * (int64_t)std::max(n_cu, 1);
+    fused = fused_fits && n_chains <= 8 * (int64_t)std::max(n_cu, 1);
   if (fused && !fused_fits) return fail(ctx, TCI_ERANGE, "tci_dram_run: rows too long for the fused engine");
   if (fused) {
-    // Chunks of chain rows up to the next adaptation row; k_chain leaves *st.step at the chunk end.
-    const int64_t G = ai > 0 ? ai : 1000;
+    // Chunks of chain rows up to the next adaptation row (and at most p.chunk rows: the draws
+    // buffer holds one chunk); k_chain leaves *st.step at the chunk end.
+    const int64_t DW = tci::draw_stride(ld);
+    const int64_t want = ai > 0 ? ai : 1000;
+    const int64_t cap = std::max<int64_t>(32, (int64_t)(((size_t)2 << 30) / (n * (size_t)DW * sizeof(double))));
+    p.chunk = std::min(want, cap);
+    st.draws = A.alloc<double>(n * (size_t)p.chunk * DW, &e);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dram draws)");
     for (int64_t next = 2; next <= opt->n_steps && rc == TCI_OK;) {
-      const int64_t end = std::min<int64_t>(opt->n_steps, ((next + G - 1) / G) * G);
+      int64_t end = std::min<int64_t>(opt->n_steps, next + p.chunk - 1);
+      if (ai > 0) end = std::min<int64_t>(end, ((next + ai - 1) / ai) * ai);
       rc = tci::dram_launch_chain(st, p, ctx->kp, ctx->rpl, next, end, s);
       if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(st, p, s);
       next = end + 1;
@@ -706,16 +718,6 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_HIP(ctx, hipStreamSynchronize(s));
   if (exec) (void)hipGraphExecDestroy(exec);
   if (graph) (void)hipGraphDestroy(graph);
-#ifdef TCI_CHAIN_PROFILE
-  {
-    int64_t ph[8];
-    TCI_HIP(ctx, hipMemcpy(ph, st.prof, sizeof(ph), hipMemcpyDeviceToHost));
-    std::fprintf(stderr, "{\"k_chain_phase_cycles_per_chain_step\": [");
-    for (int k = 0; k < 8; ++k)
-      std::fprintf(stderr, "%s%.1f", k ? ", " : "", (double)ph[k] / (double)n / (double)std::max<int64_t>(opt->n_steps - 1, 1));
-    std::fprintf(stderr, "]}\n");
-  }
-#endif
   if (ge != hipSuccess) return hip_fail(ctx, ge, "DRAM step replay");
   if (rc != TCI_OK) return fail(ctx, rc, "DRAM step launch");
   float ms = 0.f;

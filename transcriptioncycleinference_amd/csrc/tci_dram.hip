@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "tci_dram_internal.h"
 #include "tci_eval.h"
 
@@ -97,8 +99,11 @@ __device__ __forceinline__ double uniform_at(uint64_t seed, int64_t c, int64_t s
   return u01(r.x, r.y);
 }
 
-// Gamma(a, scale) by Marsaglia & Tsang (a >= 1 here: a = N/2 >= 2).
-__device__ double gamma_at(uint64_t seed, int64_t c, int64_t step, double a, double scale) {
+// Gamma(a, 1) by Marsaglia & Tsang (a >= 1 here: a = N/2 >= 2) as the product d*v; a Gamma(a, scale)
+// variate is (d*v)*scale. The unit variate depends only on the stream and a, so the fused engine
+// draws it ahead of the chain (k_draws) and the scale (2/SS of the current state) is applied when
+// it is used: the same bits as gamma_at.
+__device__ double gamma_unit(uint64_t seed, int64_t c, int64_t step, double a) {
   const double d = a - 1.0 / 3.0, cc = 1.0 / sqrt(9.0 * d);
   for (uint32_t it = 0; it < 1024; ++it) {
     const uint4 r = rng(seed, c, step, P_GAMMA, it);
@@ -110,10 +115,13 @@ __device__ double gamma_at(uint64_t seed, int64_t c, int64_t step, double a, dou
     if (v <= 0.0) continue;
     v = v * v * v;
     const double x2 = x * x;
-    if (u < 1.0 - 0.0331 * x2 * x2) return d * v * scale;  // squeeze (implies the log test)
-    if (log(u) < 0.5 * x2 + d - d * v + d * log(v)) return d * v * scale;
+    if (u < 1.0 - 0.0331 * x2 * x2) return d * v;  // squeeze (implies the log test)
+    if (log(u) < 0.5 * x2 + d - d * v + d * log(v)) return d * v;
   }
-  return a * scale;  // unreachable in practice (acceptance > 0.95 per try)
+  return a;  // unreachable in practice (acceptance > 0.95 per try)
+}
+__device__ __forceinline__ double gamma_at(uint64_t seed, int64_t c, int64_t step, double a, double scale) {
+  return gamma_unit(seed, c, step, a) * scale;
 }
 
 __device__ __forceinline__ double wsum64(double x) {
@@ -275,7 +283,7 @@ __device__ double prior_block(const double* th, const double* mu, const double* 
 __device__ bool propose_block(const DramState& st, const DramParams& p, int64_t c, int64_t step, uint32_t purpose,
                               const double* base, double scale, int P, double* out, Smem& sm) {
   const int64_t ld = st.ld;
-  draw_normals(p.seed, c, step, purpose, P, sm.z, threadIdx.x);
+  draw_normals(p.seed, st.key[c], step, purpose, P, sm.z, threadIdx.x);
   load_R_f32(sm.Rl, st.R + c * ld * ld, ld, P);
   __syncthreads();
   mfma_zr(sm.z, sm.L, 1, sm.Rl, P, sm.y, sm.L);
@@ -424,7 +432,7 @@ __global__ __launch_bounds__(kThreads) void k_accept1(DramState st, DramParams p
     pr1 = prior_block(y1, st.pmu + c * ld, st.psig + c * ld, P, sm.red);
     const double e = -0.5 * (st.ss1[c] - st.ss[c]) / st.sigma2[c] - 0.5 * (pr1 - st.prior[c]);
     a12 = fmin(1.0, exp(e));
-    acc = uniform_at(p.seed, c, step, P_U1) < a12;
+    acc = uniform_at(p.seed, st.key[c], step, P_U1) < a12;
   }
   if (acc) {
     for (int j = threadIdx.x; j < P; j += kThreads) th[j] = y1[j];
@@ -464,12 +472,12 @@ __global__ __launch_bounds__(kThreads) void k_accept2(DramState st, DramParams p
     // ss1 = +Inf (stage 1 out of bounds) gives alpha32 = 0, alpha12 = 0
     const double a32 = fmin(1.0, exp(-0.5 * (ss1 - ss2) / s2 - 0.5 * (st.prior1[c] - pr2)));
     const double l2 = exp(-0.5 * (ss2 - st.ss[c]) / s2 - 0.5 * (pr2 - st.prior[c]));
-    draw_normals(p.seed, c, step, P_NORM1, P, sm.z, threadIdx.x);
-    draw_normals(p.seed, c, step, P_NORM2, P, sm.y, threadIdx.x);
+    draw_normals(p.seed, st.key[c], step, P_NORM1, P, sm.z, threadIdx.x);
+    draw_normals(p.seed, st.key[c], step, P_NORM2, P, sm.y, threadIdx.x);
     __syncthreads();
     const double q1 = dr_q1(sm.z, sm.y, 1.0 / p.drscale, P, sm.red);
     const double a13 = l2 * q1 * (1.0 - a32) / (1.0 - a12);
-    acc2 = uniform_at(p.seed, c, step, P_U2) < a13;
+    acc2 = uniform_at(p.seed, st.key[c], step, P_U2) < a13;
     if (acc2) {
       for (int j = threadIdx.x; j < P; j += kThreads) th[j] = y2[j];
       if (threadIdx.x == 0) {
@@ -482,7 +490,7 @@ __global__ __launch_bounds__(kThreads) void k_accept2(DramState st, DramParams p
   if (threadIdx.x == 0) {
     if (!(st.acc1[c] != 0 || acc2)) st.nrej_win[c] += 1;  // no stage moved the chain
     // sigma2 Gibbs update (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/oldss)
-    if (p.updatesigma) st.sigma2[c] = 1.0 / gamma_at(p.seed, c, step, 0.5 * (double)st.nobs[c], 2.0 / st.ss[c]);
+    if (p.updatesigma) st.sigma2[c] = 1.0 / gamma_at(p.seed, st.key[c], step, 0.5 * (double)st.nobs[c], 2.0 / st.ss[c]);
   }
   __syncthreads();
   record_row(st, p, c, step, P, st.theta + c * st.ld, st.sigma2[c]);
@@ -598,37 +606,19 @@ __global__ __launch_bounds__(kThreads) void k_adapt(DramState st, DramParams p) 
 }
 
 
-// ---- Fused chain engine: one workgroup runs chain rows s_begin..s_end of its chain with every
-// ssfun evaluation inside the loop (no launch per step). Waves 0 and 1 evaluate the stage-1
-// proposal and the stage-2 proposal concurrently (stage 2 is drawn up front from its own stream
-// and used only when stage 1 rejects, so nothing changes but the latency). Adaptation stays the
-// k_adapt launch between chunks. Same RNG keys, reductions and operation order as the batched
-// engine above: the two engines produce identical chains (tests/test_dram_gpu.py).
-
-#ifndef TCI_CHAIN_PROFILE
-#define TCI_CHAIN_PROFILE 0  // diagnostics: per-phase s_memtime cycles of k_chain into st.prof
-#endif
-__device__ __forceinline__ uint64_t stamp() {
-#if TCI_CHAIN_PROFILE
-  uint64_t t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-#else
-  return 0;
-#endif
-}
-
-// Steps per proposal block of k_chain: the normals of kBlockSteps steps (2 stages each: 8 rows)
-// are drawn together and multiplied by R in one pass of MFMA tiles.
-constexpr int kBlockSteps = 4;
-
-// Dynamic LDS bytes of k_chain for vector stride L (>= P): 9 vectors, the block's normals and
-// products (2 x 8 rows), red, and the chain's R as packed fp32 (constant over a chunk).
-__host__ __device__ inline int64_t chain_lds_bytes(int64_t L) {
-  return (9 * L + 4 * kBlockSteps * L + 8) * 8 + (L * (L + 1) / 2) * 4 + 16;
-}
+// ---- Fused chain engine. Per chunk of chain rows between two adaptations (R fixed):
+//   k_draws  every random quantity of the chunk that does not depend on the chain state, for all
+//            chains and steps in one wide launch: the proposal offsets u1 = z1*R and u2 = z2*R
+//            (MFMA tiles of 8 steps x 2 stages), the delayed-rejection norms |z2/drscale - z1|^2
+//            and |z1|^2, the two acceptance uniforms and the unit Gamma variate of the sigma2 draw;
+//   k_chain  one workgroup per chain walks the chunk's rows with ONE workgroup barrier per step:
+//            waves 0 and 1 evaluate ssfun at the stage-1 and stage-2 proposals concurrently (stage
+//            2 is used only when stage 1 rejects, so only the latency changes), wave 2 computes the
+//            priors and records the previous row, wave 3 records the previous sigma2. Every wave
+//            keeps its own copy of theta in registers and takes the same acceptance decision from
+//            the values exchanged at the barrier; the next step's draws are prefetched meanwhile.
+// Same RNG keys, reductions and operation order as the batched engine above: the two engines
+// produce identical chains (tests/test_dram_gpu.py).
 
 // Normals of both stages for `ns` steps from `step` into rows 2 k (stage 1, P_NORM1) and 2 k + 1
 // (stage 2, P_NORM2) of Z (row stride L), one Box-Muller pair per thread and round.
@@ -650,41 +640,163 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
   }
 }
 
-template <int RPL, int NSEG>
-__global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
-                                                    int64_t s_end) {
-  constexpr int EV = eval_lds_doubles<RPL>();
-  __shared__ __attribute__((aligned(16))) double evl[2][EV];
-  __shared__ double ssv[2];
+constexpr int kDrawSteps = 8;  // steps per MFMA row tile (2 rows per step: 16 rows)
+constexpr int kDrawTiles = 4;  // row tiles per k_draws workgroup (32 steps)
+enum DrawSlot { D_Q21 = 0, D_Q01 = 1, D_U1 = 2, D_U2 = 3, D_G = 4 };
+
+// Dynamic LDS of k_draws: the tile's normals and products (2 x 16 rows of stride L) and the chain's
+// R as packed fp32.
+__host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
+  return (2 * 2 * kDrawSteps * L) * 8 + (L * (L + 1) / 2) * 4 + 16;
+}
+
+__global__ __launch_bounds__(kThreads) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end) {
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int64_t ld = st.ld;
   const int L = (int)ld;
   const int P = st.npar[c];
-  double* y1 = dyn;
-  double* y2 = y1 + L;
-  double* th = y2 + L;
-  double* lo = th + L;
-  double* hi = lo + L;
-  double* mu = hi + L;
-  double* sg = mu + L;
-  double* smn = sg + L;                     // posterior Welford mean / M2 of the chain (this chunk)
-  double* sm2 = smn + L;
-  double* Zb = sm2 + L;                     // 2*kBlockSteps normal rows (stage 1, stage 2 per step)
-  double* Ub = Zb + 2 * kBlockSteps * L;    // their products with R
-  double* red = Ub + 2 * kBlockSteps * L;   // [0..3]: prior1, prior2, q21, q01; [4]: sigma2
-  float* Rl = reinterpret_cast<float*>(red + 8);
+  const int64_t key = st.key[c];
+  const int64_t DW = draw_stride(ld);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  double* Z = dyn;
+  double* U = Z + 2 * kDrawSteps * L;
+  float* Rl = reinterpret_cast<float*>(U + 2 * kDrawSteps * L);
   load_R_f32(Rl, st.R + c * ld * ld, ld, P);
-  for (int j = t; j < P; j += kThreads) {
-    th[j] = st.theta[c * ld + j];
-    lo[j] = st.lower[c * ld + j];
-    hi[j] = st.upper[c * ld + j];
-    mu[j] = st.pmu[c * ld + j];
-    sg[j] = st.psig[c * ld + j];
-    smn[j] = st.smean[c * ld + j];
-    sm2[j] = st.sm2[c * ld + j];
+  const double a = 0.5 * (double)st.nobs[c];
+  const double inv_ds = 1.0 / p.drscale;
+  for (int tile = 0; tile < kDrawTiles; ++tile) {
+    const int64_t step0 = s_begin + ((int64_t)blockIdx.y * kDrawTiles + tile) * kDrawSteps;
+    if (step0 > s_end) break;  // uniform over the workgroup
+    const int ns = (int)min<int64_t>(kDrawSteps, s_end - step0 + 1);
+    draw_block_normals(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
+    __syncthreads();  // (the first tile: also R)
+    mfma_zr(Z, L, 2 * ns, Rl, P, U, L);
+    double* d0 = st.draws + (c * p.chunk + (step0 - s_begin)) * DW;
+    for (int k = 0; k < ns; ++k)
+      for (int j = threadIdx.x; j < P; j += kThreads) {
+        d0[k * DW + j] = U[2 * k * L + j];
+        d0[k * DW + ld + j] = U[(2 * k + 1) * L + j];
+      }
+    for (int k = w; k < ns; k += kThreads / 64) {
+      const int64_t step = step0 + k;
+      const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
+      if (lane == 0) {
+        double* sc = d0 + k * DW + 2 * ld;
+        sc[D_Q21] = q.x;
+        sc[D_Q01] = q.y;
+        sc[D_U1] = uniform_at(p.seed, key, step, P_U1);
+        sc[D_U2] = uniform_at(p.seed, key, step, P_U2);
+        sc[D_G] = p.updatesigma ? gamma_unit(p.seed, key, step, a) : 1.0;
+      }
+    }
+    __syncthreads();  // Z and U are rewritten by the next tile
+  }
+}
+
+// One chain row's draws (this lane's vector entries j = lane + 64 k and the scalars).
+template <int NJ>
+struct StepDraws {
+  double u1[NJ], u2[NJ];
+  double q21, q01, U1, U2, G;
+};
+template <int NJ>
+__device__ __forceinline__ void load_draws(StepDraws<NJ>& d, const double* __restrict__ src, int64_t ld, int P,
+                                           int lane) {
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    const int j = lane + 64 * k;
+    d.u1[k] = j < P ? src[j] : 0.0;
+    d.u2[k] = j < P ? src[ld + j] : 0.0;
+  }
+  const double* sc = src + 2 * ld;
+  d.q21 = sc[D_Q21];
+  d.q01 = sc[D_Q01];
+  d.U1 = sc[D_U1];
+  d.U2 = sc[D_U2];
+  d.G = sc[D_G];
+}
+
+// wave_prior on register-held vectors (entry k of lane l is j = l + 64 k): the same per-lane
+// order and shuffle tree, so the same bits.
+template <int NJ>
+__device__ __forceinline__ double wave_prior_reg(const double* y, const double* mu, const double* sg, int P, int lane) {
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    if (lane + 64 * k < P && isfinite(sg[k])) {
+      const double z = (y[k] - mu[k]) / sg[k];
+      s += z * z;
+    }
+  }
+  return wsum64(s);
+}
+
+// record_vec on register-held vectors by one wave (smn/sm2: this lane's Welford entries).
+template <int NJ>
+__device__ __forceinline__ void record_vec_reg(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P,
+                                               const double* th, double* smn, double* sm2, int lane) {
+  const int64_t ld = st.ld;
+  if (p.adaptint > 0) {
+    double* w = st.window + (c * p.adaptint + (row - 1) % p.adaptint) * ld;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k)
+      if (lane + 64 * k < P) w[lane + 64 * k] = th[k];
+  }
+  if (row >= p.stats_from) {
+    const double n = (double)(row - p.stats_from + 1);
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      if (lane + 64 * k < P) {
+        const double x = th[k];
+        double m = smn[k];
+        const double d = x - m;
+        m += d / n;
+        smn[k] = m;
+        sm2[k] += d * (x - m);
+      }
+    }
+  }
+  if (st.chain_out != nullptr && p.thin > 0 && (row - 1) % p.thin == 0) {
+    const int64_t kk = (row - 1) / p.thin;
+    if (kk < p.n_keep)
+#pragma unroll
+      for (int k = 0; k < NJ; ++k)
+        if (lane + 64 * k < P) st.chain_out[(kk * st.n_chains + c) * ld + lane + 64 * k] = th[k];
+  }
+}
+
+template <int RPL, int NSEG>
+__global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
+                                                    int64_t s_end) {
+  constexpr int NJ = RPL + 1;  // vector entries per lane: P = 7 + N <= 64 RPL + 8 <= 64 NJ
+  constexpr int EV = eval_lds_doubles<RPL>();
+  __shared__ __attribute__((aligned(16))) double evl[2][EV];  // the two evaluating waves' tables
+  __shared__ double yl[2][64 * NJ];                            // the proposal each of them evaluates
+  __shared__ double xch[2][4];  // by step parity: ss1, ss2, prior1, prior2
+  const int64_t c = blockIdx.x;
+  if (c >= st.n_chains) return;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t ld = st.ld;
+  const int P = st.npar[c];
+  const int64_t DW = draw_stride(ld);
+  const double* drow = st.draws + c * p.chunk * DW - s_begin * DW;  // row of step s: drow + s * DW
+  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], smn[NJ], sm2[NJ];
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    const int j = lane + 64 * k;
+    const bool in = j < P;
+    th[k] = in ? st.theta[c * ld + j] : 0.0;
+    lo[k] = in ? st.lower[c * ld + j] : 0.0;
+    hi[k] = in ? st.upper[c * ld + j] : 0.0;
+    mu[k] = sg[k] = smn[k] = sm2[k] = 0.0;
+    if (w == 2 && in) {
+      mu[k] = st.pmu[c * ld + j];
+      sg[k] = st.psig[c * ld + j];
+      smn[k] = st.smean[c * ld + j];
+      sm2[k] = st.sm2[c * ld + j];
+    }
   }
   // the chain's cell records stay in the registers of the two evaluating waves
   EvalIn<RPL> e;
@@ -705,158 +817,142 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   if (w == 3) s2a = S2Stats{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
   int32_t nacc = st.naccept[c], nrej = st.nrej_win[c];
   int64_t nev = st.nevals[c];
-  const double half_nobs = 0.5 * (double)st.nobs[c];
   const double scale2 = 1.0 / p.drscale;
-  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t t0 = stamp(), t1;
-#define TCI_PHASE(k) \
-  if (TCI_CHAIN_PROFILE) { t1 = stamp(); ph[k] += t1 - t0; t0 = t1; }
-  __syncthreads();
+  StepDraws<NJ> d;
+  load_draws<NJ>(d, drow + s_begin * DW, ld, P, lane);
   for (int64_t step = s_begin; step <= s_end; ++step) {
-    // ---- proposals: stage 1 theta + z1*R, stage 2 theta + z2*R/drscale (both drawn up front,
-    //      kBlockSteps steps at a time: the products are state-independent)
-    const int sl = (int)((step - s_begin) % kBlockSteps);
-    if (sl == 0) {
-      const int ns = (int)min<int64_t>(kBlockSteps, s_end - step + 1);
-      draw_block_normals(p.seed, c, step, ns, P, p.ntry >= 2, Zb, L);
-      __syncthreads();
-      TCI_PHASE(0)
-      mfma_zr(Zb, L, 2 * ns, Rl, P, Ub, L);
-      TCI_PHASE(1)
+    const int par = (int)(step & 1);
+    StepDraws<NJ> dn;  // the next row's draws, in flight during this step
+    load_draws<NJ>(dn, drow + (step < s_end ? step + 1 : step) * DW, ld, P, lane);
+    // ---- proposals: stage 1 theta + z1*R, stage 2 theta + z2*R/drscale; bounds by wave vote
+    double y1[NJ], y2[NJ];
+    bool out1 = false, out2 = false;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      y1[k] = th[k] + 1.0 * d.u1[k];
+      y2[k] = th[k] + scale2 * d.u2[k];
+      if (lane + 64 * k < P) {
+        out1 |= !(y1[k] >= lo[k] && y1[k] <= hi[k]);
+        out2 |= !(y2[k] >= lo[k] && y2[k] <= hi[k]);
+      }
     }
-    const double* z1 = Zb + (2 * sl) * L;
-    const double* z2 = Zb + (2 * sl + 1) * L;
-    const double* u1 = Ub + (2 * sl) * L;
-    const double* u2 = Ub + (2 * sl + 1) * L;
-    int ok1 = 1, ok2 = 1;
-    for (int j = t; j < P; j += kThreads) {
-      const double a = th[j] + 1.0 * u1[j];
-      const double b = th[j] + scale2 * u2[j];
-      y1[j] = a;
-      y2[j] = b;
-      ok1 &= (a >= lo[j] && a <= hi[j]) ? 1 : 0;
-      ok2 &= (b >= lo[j] && b <= hi[j]) ? 1 : 0;
-    }
-    const bool inb1 = __syncthreads_and(ok1) != 0;
-    const bool inb2 = __syncthreads_and(ok2) != 0 && p.ntry >= 2;
-    TCI_PHASE(2)
-    // ---- one phase, four waves: ssfun of both proposals (waves 0, 1; out of bounds: not called,
-    //      +Inf); priors and the delayed-rejection sums (wave 2); the previous row's record and
-    //      sigma2 Gibbs draw (waves 2, 3; sigma2 is first used by this step's acceptance).
+    const bool inb1 = wave_ballot(out1) == 0;
+    const bool inb2 = wave_ballot(out2) == 0 && p.ntry >= 2;
+    // ---- ssfun at both proposals (waves 0, 1; out of bounds: not called, +Inf), the priors and
+    //      the previous row's record (wave 2), the previous row's sigma2 record (wave 3)
     if (w < 2) {
-      const double* yy = w == 0 ? y1 : y2;
       double r = INFINITY;
       if (w == 0 ? inb1 : inb2) {
-        e.v = yy[0];
-        e.tau = yy[1];
-        e.ton = yy[2];
-        e.b1 = yy[3];
-        e.b2 = yy[4];
-        e.A = yy[5];
-        e.R = yy[6];
+        double* yb = yl[w];
+#pragma unroll
+        for (int k = 0; k < NJ; ++k) yb[lane + 64 * k] = w == 0 ? y1[k] : y2[k];
+        wave_sync();
+        e.v = yb[0];
+        e.tau = yb[1];
+        e.ton = yb[2];
+        e.b1 = yb[3];
+        e.b2 = yb[4];
+        e.A = yb[5];
+        e.R = yb[6];
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
           const int g = RPL * lane + q;
-          e.dr[q] = 7 + g < P ? yy[7 + g] : 0.0;
+          e.dr[q] = 7 + g < P ? yb[7 + g] : 0.0;
         }
         r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
       }
-      if (lane == 0) ssv[w] = r;
+      if (lane == 0) xch[par][w] = r;
     } else if (w == 2) {
-      const double pr1 = wave_prior(y1, mu, sg, P, lane);
-      const double pr2 = wave_prior(y2, mu, sg, P, lane);
-      const double2 q = wave_q(z1, z2, scale2, P, lane);
+      const double pr1 = inb1 ? wave_prior_reg<NJ>(y1, mu, sg, P, lane) : 0.0;
+      const double pr2 = inb2 ? wave_prior_reg<NJ>(y2, mu, sg, P, lane) : 0.0;
       if (lane == 0) {
-        red[0] = pr1;
-        red[1] = pr2;
-        red[2] = q.x;
-        red[3] = q.y;
+        xch[par][2] = pr1;
+        xch[par][3] = pr2;
       }
-      if (step > s_begin) record_vec(st, p, c, step - 1, P, th, smn, sm2, lane, 64);
-    } else {
-      if (step > s_begin) {
-        if (p.updatesigma) s2 = 1.0 / gamma_at(p.seed, c, step - 1, half_nobs, 2.0 / ss);
-        if (lane == 0) record_s2(st, p, c, step - 1, s2, s2a);
-      }
-      if (lane == 0) red[4] = s2;
+      if (step > s_begin) record_vec_reg<NJ>(st, p, c, step - 1, P, th, smn, sm2, lane);
+    } else if (step > s_begin && lane == 0) {
+      record_s2(st, p, c, step - 1, s2, s2a);
     }
     __syncthreads();
-    TCI_PHASE(3)
-    const double ss1 = ssv[0], ss2 = ssv[1];
-    s2 = red[4];
+    const double ss1 = xch[par][0], ss2 = xch[par][1];
     // ---- stage 1 (k_accept1)
     double a12 = 0.0, pr1 = 0.0;
     bool acc = false;
     if (inb1) {
       nev += 1;
-      pr1 = red[0];
+      pr1 = xch[par][2];
       const double ex = -0.5 * (ss1 - ss) / s2 - 0.5 * (pr1 - prior);
       a12 = fmin(1.0, exp(ex));
-      acc = uniform_at(p.seed, c, step, P_U1) < a12;
+      acc = d.U1 < a12;
     }
     // ---- stage 2 (k_accept2)
     bool acc2 = false;
     double pr2 = 0.0;
     if (!acc && inb2) {
       nev += 1;
-      pr2 = red[1];
+      pr2 = xch[par][3];
       const double a32 = fmin(1.0, exp(-0.5 * (ss1 - ss2) / s2 - 0.5 * (pr1 - pr2)));
       const double l2 = exp(-0.5 * (ss2 - ss) / s2 - 0.5 * (pr2 - prior));
-      const double q1 = exp(-0.5 * (red[2] - red[3]));
+      const double q1 = exp(-0.5 * (d.q21 - d.q01));
       const double a13 = l2 * q1 * (1.0 - a32) / (1.0 - a12);
-      acc2 = uniform_at(p.seed, c, step, P_U2) < a13;
+      acc2 = d.U2 < a13;
     }
-    __syncthreads();  // red[] and th are rewritten below / next step
     if (acc || acc2) {
-      const double* yy = acc ? y1 : y2;
-      for (int j = t; j < P; j += kThreads) th[j] = yy[j];
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) th[k] = acc ? y1[k] : y2[k];
       ss = acc ? ss1 : ss2;
       prior = acc ? pr1 : pr2;
       nacc += 1;
     } else {
       nrej += 1;
     }
-    TCI_PHASE(4)
+    // sigma2 Gibbs update of this row (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/ss)
+    if (p.updatesigma) s2 = 1.0 / (d.G * (2.0 / ss));
+    d = dn;
   }
-  // the last row of the chunk: sigma2 draw and record
-  if (p.updatesigma) s2 = 1.0 / gamma_at(p.seed, c, s_end, half_nobs, 2.0 / ss);
-  __syncthreads();
-  record_vec(st, p, c, s_end, P, th, smn, sm2, t, kThreads);
-  if (w == 3 && lane == 0) record_s2(st, p, c, s_end, s2, s2a);
-  __syncthreads();
-  for (int j = t; j < P; j += kThreads) {
-    st.smean[c * ld + j] = smn[j];
-    st.sm2[c * ld + j] = sm2[j];
-  }
-  if (w == 3 && lane == 0) {
+  // the last row of the chunk
+  if (w == 2) {
+    record_vec_reg<NJ>(st, p, c, s_end, P, th, smn, sm2, lane);
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      const int j = lane + 64 * k;
+      if (j < P) {
+        st.smean[c * ld + j] = smn[k];
+        st.sm2[c * ld + j] = sm2[k];
+      }
+    }
+  } else if (w == 3 && lane == 0) {
+    record_s2(st, p, c, s_end, s2, s2a);
     st.s2sum[c] = s2a.sum;
     st.sq_mean[c] = s2a.qmean;
     st.sq_m2[c] = s2a.qm2;
-  }
-#undef TCI_PHASE
-  if (TCI_CHAIN_PROFILE && t == 0 && st.prof != nullptr)
-    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&st.prof[k], (unsigned long long)ph[k]);
-  for (int j = t; j < P; j += kThreads) st.theta[c * ld + j] = th[j];
-  if (t == 0) {
-    st.ss[c] = ss;
-    st.prior[c] = prior;
-    st.sigma2[c] = s2;
-    st.naccept[c] = nacc;
-    st.nrej_win[c] = nrej;
-    st.nevals[c] = nev;
-    if (c == 0) *st.step = s_end;  // k_adapt reads the row it follows
+  } else if (w == 0) {
+#pragma unroll
+    for (int k = 0; k < NJ; ++k)
+      if (lane + 64 * k < P) st.theta[c * ld + lane + 64 * k] = th[k];
+    if (lane == 0) {
+      st.ss[c] = ss;
+      st.prior[c] = prior;
+      st.sigma2[c] = s2;
+      st.naccept[c] = nacc;
+      st.nrej_win[c] = nrej;
+      st.nevals[c] = nev;
+      if (c == 0) *st.step = s_end;  // k_adapt reads the row it follows
+    }
   }
 }
 
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    hipStream_t stream) {
-  const size_t lds = (size_t)chain_lds_bytes(st.ld);
+  const size_t lds = (size_t)draws_lds_bytes(st.ld);
   if (lds > 48 * 1024 &&
-      hipFuncSetAttribute((const void*)k_chain<RPL, NSEG>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-          hipSuccess)
+      hipFuncSetAttribute((const void*)k_draws, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return TCI_EHIP;
-  hipLaunchKernelGGL((k_chain<RPL, NSEG>), dim3((unsigned)st.n_chains), dim3(kThreads), lds, stream, st, p, kp,
+  const int64_t per_wg = (int64_t)kDrawSteps * kDrawTiles;
+  const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
+  hipLaunchKernelGGL(k_draws, dim3((unsigned)st.n_chains, gy), dim3(kThreads), lds, stream, st, p, s_begin, s_end);
+  hipLaunchKernelGGL((k_chain<RPL, NSEG>), dim3((unsigned)st.n_chains), dim3(kThreads), 0, stream, st, p, kp,
                      s_begin, s_end);
   return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;
 }
@@ -1166,7 +1262,8 @@ int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& k
   }
 }
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl) {
-  return chain_lds_bytes(ld) + 2 * (4 * 64 * rpl + 4 * rpl) * 8 + 64;
+  const int64_t chain = 2 * (4 * 64 * rpl + 4 * rpl) * 8 + 2 * 64 * (rpl + 1) * 8 + 64;  // k_chain (static)
+  return std::max<int64_t>(chain, draws_lds_bytes(ld));                                  // k_draws (dynamic)
 }
 int dram_launch_step_incr(const DramState& st, void* stream) {
   hipLaunchKernelGGL(k_step_incr, dim3(1), dim3(64), 0, (hipStream_t)stream, st.step);

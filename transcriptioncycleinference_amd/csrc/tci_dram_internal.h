@@ -14,6 +14,7 @@ struct DramState {
   int64_t n_chains;
   int64_t ld;
   const int32_t* cell;     // chain -> cell of the context
+  const int64_t* key;      // chain -> RNG stream key (tci_dram_options.chain_keys; identity when absent)
   const int32_t* npar;     // P_c = 7 + N_c
   const int32_t* nobs;     // N = length(ydata) = 2 N_c (TranscriptionCycleMCMC.m:260)
   const double* lower;     // bounds (TranscriptionCycleMCMC.m:242-255)
@@ -50,8 +51,12 @@ struct DramState {
   double* s2_out;          // optional thinned s2 rows
   double* work;            // Cholesky workspace (n_chains x ld x ld)
   int64_t* step;           // current chain row (1-based), advanced on device after each step
-  int64_t* prof;           // TCI_CHAIN_PROFILE builds only: cycles per k_chain phase, summed over chains
+  double* draws;           // fused engine: per chain, p.chunk rows of draw_stride(ld) doubles (k_draws)
 };
+
+// One chain row's state-independent draws (fused engine): u1 = z1*R [ld], u2 = z2*R [ld], then
+// the scalars |z2/drscale - z1|^2, |z1|^2, the two acceptance uniforms and the unit Gamma variate.
+constexpr int64_t draw_stride(int64_t ld) { return 2 * ld + 8; }
 
 struct DramParams {
   uint64_t seed;
@@ -68,6 +73,7 @@ struct DramParams {
   int64_t n_keep;
   int64_t lds_matrix;  // bytes of dynamic LDS for the adaptation matrix (0 = work in global memory)
   int64_t pmax;        // max parameter count over the chains (picks the adaptation kernel)
+  int64_t chunk;       // fused engine: rows per chain of the draws buffer (>= the longest chunk)
 };
 
 int dram_launch_init(const DramState& st, const double* qcov_diag, const double* sigma2_0, void* stream);

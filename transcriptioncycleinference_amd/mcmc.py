@@ -11,7 +11,7 @@ Mirrors ``src/TranscriptionCycleMCMC.m``:
   skipped cells (``:359-369``) and the two result files (``:371-378``).
 
 The reference runs cells in a parfor with independent MATLAB RNG streams (``rand``/``normrnd``).
-Here x0 comes from ``numpy.random.default_rng(seed)`` and the chains from Philox streams, so a
+Here x0 comes from ``numpy.random.default_rng([seed, cell])`` and the chains from Philox streams, so a
 fit reproduces the reference's *distribution*, not its exact draws.
 """
 from __future__ import annotations
@@ -57,14 +57,15 @@ class DramOptions:
 
     ENGINES = {"auto": 0, "fused": 1, "batched": 2}
 
-    def to_c(self) -> "_lib.tci_dram_options":
+    def to_c(self, chain_keys: Optional[np.ndarray] = None) -> "_lib.tci_dram_options":
+        """``chain_keys`` (int64 [n_chains], kept alive by the caller): chain c's RNG stream key."""
         if self.engine not in self.ENGINES:
             raise ValueError(f"engine must be one of {sorted(self.ENGINES)}, got {self.engine!r}")
         return _lib.tci_dram_options(int(self.n_steps), int(self.burnintime), int(self.adaptint), int(self.ntry),
                                      int(bool(self.updatesigma)), float(self.drscale), float(self.adascale),
                                      float(self.qcovadj), float(self.burnin_scale), int(self.stats_from),
                                      int(self.thin), int(self.seed) & 0xFFFFFFFFFFFFFFFF,
-                                     self.ENGINES[self.engine], 0)
+                                     self.ENGINES[self.engine], 0, _lib.ptr(chain_keys, _lib._i64p))
 
 
 @dataclass
@@ -83,9 +84,10 @@ class DramResult:
 
 
 def dram_run(lk, cell_id, theta0, lower, upper, prior_mu, prior_sig, qcov_diag, sigma2_0,
-             opts: DramOptions, want_qcov: bool = False) -> DramResult:
+             opts: DramOptions, want_qcov: bool = False, chain_keys=None) -> DramResult:
     """Run one chain per row on the device (``tci_dram_run``). Arrays are (n_chains, ld).
-    ``want_qcov``: also return the final proposal factor R (n_chains, ld, ld)."""
+    ``want_qcov``: also return the final proposal factor R (n_chains, ld, ld). ``chain_keys``:
+    RNG stream key per chain (default: the row index)."""
     f = lambda a: np.ascontiguousarray(a, np.float64)  # noqa: E731
     theta0, lower, upper, prior_mu, prior_sig, qcov_diag = map(f, (theta0, lower, upper, prior_mu, prior_sig,
                                                                     qcov_diag))
@@ -103,7 +105,10 @@ def dram_run(lk, cell_id, theta0, lower, upper, prior_mu, prior_sig, qcov_diag, 
                                 _lib.ptr(smean, _lib._dp), _lib.ptr(sstd, _lib._dp), _lib.ptr(acc, _lib._dp),
                                 _lib.ptr(nev, _lib._i64p), _lib.ptr(chain, _lib._dp), _lib.ptr(s2c, _lib._dp),
                                 _lib.ptr(qR, _lib._dp), 0.0)
-    o = opts.to_c()
+    keys = None if chain_keys is None else np.ascontiguousarray(chain_keys, np.int64)
+    if keys is not None and keys.shape != (n,):
+        raise ValueError("chain_keys must have one entry per chain")
+    o = opts.to_c(keys)
     P = lambda a: _lib.ptr(a, _lib._dp)  # noqa: E731
     lk._check(lk._lib.tci_dram_run(lk._h, C.byref(o), n, _lib.ptr(cid, _lib._i32p), P(theta0), P(lower), P(upper),
                                    P(prior_mu), P(prior_sig), P(qcov_diag), P(s20), ld, C.byref(out)))
@@ -154,17 +159,20 @@ def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 5
     previous fit (loadPrevious, :193-198); cells whose v0 is None/NaN are skipped (``continue``,
     :196-198) and pruned from the outputs (:359-369). ``thin``: keep every thin-th raw chain row
     in ``MCMCchain`` (the reference keeps all rows from n_burn, :276-283 -- ~193 MB/cell at 200k
-    steps; thin=1 reproduces that)."""
+    steps; thin=1 reproduces that). ``cells``: fit only these cell indices (a shard).
+
+    Everything random is keyed by the cell index -- x0 by ``default_rng([seed, cell])``, the chain
+    by RNG stream ``cell`` -- so fitting a subset of the cells (one GPU's shard,
+    :func:`parallel.fit_sharded`) reproduces those cells' results of the full fit bit for bit."""
     cl: Cells = lk.cells
     ids = list(range(cl.n_cells)) if cells is None else [int(c) for c in cells]
-    rng = np.random.default_rng(seed)
     rows, keep = [], []
     for k, c in enumerate(ids):
         t = cl.cell(c)[0]
         vv = None if v0 is None else v0[k]
         if v0 is not None and (vv is None or not np.isfinite(vv)):
             continue
-        rows.append(cell_setup(t, rng, ratePriorWidth, vv))
+        rows.append(cell_setup(t, np.random.default_rng([int(seed), c]), ratePriorWidth, vv))
         keep.append(c)
     if not keep:
         return FitResult(cl.name, [], [], [], np.zeros(0), 0, 0.0)
@@ -181,7 +189,7 @@ def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 5
     o = opts or DramOptions()
     o.n_steps, o.burnintime, o.stats_from, o.thin = int(n_steps), int(n_burn), int(max(n_burn, 1)), int(thin)
     o.seed = int(seed) * 1000003 + 20201028
-    res = dram_run(lk, np.array(keep, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o)
+    res = dram_run(lk, np.array(keep, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, chain_keys=np.array(keep, np.int64))
     # forward model at the means on the raw times (:307-309)
     ms2, pp7 = lk.forward(res.mean, np.array(keep, np.int32), grid="raw")
     results, plots, chains = [], [], []

@@ -63,3 +63,85 @@ def gather_rows(local: np.ndarray, group=None, device: Optional[str] = None) -> 
     parts = [o[:c].cpu().numpy() for o, c in zip(outs, counts)]
     res = np.concatenate(parts, axis=0) if parts else np.zeros((0, width))
     return res.reshape((-1,) + local.shape[1:]) if local.ndim > 1 else res.reshape(-1)
+
+
+# ---------------------------------------------------------------------------
+# Sharded fit: the parfor over cells (TranscriptionCycleMCMC.m:161) across GPUs
+# ---------------------------------------------------------------------------
+
+_SCALARS = ("mean_v", "sigma_v", "mean_ton", "sigma_ton", "mean_A", "sigma_A", "mean_tau", "sigma_tau",
+            "mean_MS2_basal", "sigma_MS2_basal", "mean_PP7_basal", "sigma_PP7_basal", "mean_R", "sigma_R",
+            "mean_sigma", "sigma_sigma")
+
+
+def pack_results(fr, n_max: int) -> np.ndarray:
+    """One float64 row per fitted cell: cell_index, ApprovedFits, N, accept rate, the 16 scalar
+    summaries, then mean_dR, sigma_dR, simMS2, simPP7 (each padded to ``n_max``): the per-cell
+    output of the reference's parfor body (:315-356) as a fixed-width row for one all-gather."""
+    k = len(fr.MCMCresults)
+    out = np.full((k, 4 + len(_SCALARS) + 4 * n_max), np.nan)
+    for i, (r, pl) in enumerate(zip(fr.MCMCresults, fr.MCMCplot)):
+        n = len(r["mean_dR"])
+        out[i, 0], out[i, 1], out[i, 2], out[i, 3] = r["cell_index"], r["ApprovedFits"], n, fr.accept_rate[i]
+        out[i, 4:4 + len(_SCALARS)] = [r[f] for f in _SCALARS]
+        base = 4 + len(_SCALARS)
+        for j, v in enumerate((r["mean_dR"], r["sigma_dR"], pl["simMS2"], pl["simPP7"])):
+            out[i, base + j * n_max:base + j * n_max + n] = v
+    return out
+
+
+def unpack_results(rows: np.ndarray, cells, dataset_name: str, n_evals: int, elapsed_ms: float):
+    """Inverse of :func:`pack_results` over the gathered rows (any rank order): a ``FitResult``
+    sorted by cell, with ``MCMCplot``'s data columns restored from ``cells``. Raw chains are not
+    gathered (``MCMCchain`` entries are empty): they stay on the rank that sampled them."""
+    from .mcmc import FitResult
+
+    rows = rows[np.argsort(rows[:, 0], kind="stable")]
+    n_max = (rows.shape[1] - 4 - len(_SCALARS)) // 4
+    results, plots, chains = [], [], []
+    base = 4 + len(_SCALARS)
+    for row in rows:
+        c, n = int(row[0]) - 1, int(row[2])
+        r = {f: float(v) for f, v in zip(_SCALARS, row[4:base])}
+        r["mean_dR"] = row[base:base + n].copy()
+        r["sigma_dR"] = row[base + n_max:base + n_max + n].copy()
+        r["cell_index"], r["ApprovedFits"] = c + 1, int(row[1])
+        from .mcmc import RESULT_FIELDS
+
+        results.append({f: r[f] for f in RESULT_FIELDS})
+        t, m, p = cells.cell(c)
+        plots.append({"t_plot": t.copy(), "MS2_plot": m.copy(), "PP7_plot": p.copy(),
+                      "simMS2": row[base + 2 * n_max:base + 2 * n_max + n].copy(),
+                      "simPP7": row[base + 3 * n_max:base + 3 * n_max + n].copy()})
+        chains.append({})
+    return FitResult(dataset_name, results, plots, chains, rows[:, 3].copy(), int(n_evals), float(elapsed_ms),
+                     (rows[:, 0].astype(np.int64) - 1))
+
+
+def fit_sharded(lk, group=None, device: Optional[str] = None, v0=None, **fit_kwargs):
+    """``TranscriptionCycleMCMC`` over ``torch.distributed`` ranks, one GPU each: rank r fits the
+    contiguous cell range ``shard_bounds`` gives it (its own GPU-resident DRAM chains), then ONE
+    all-gather of the packed per-cell results (RCCL on GPUs, gloo on CPU) gives every rank the
+    whole dataset's ``MCMCresults`` / ``MCMCplot``. The chains' randomness is keyed by cell index
+    (:func:`mcmc.fit`), so the gathered results equal a one-GPU fit of all cells bit for bit.
+    ``v0``: per-cell previous rates over ALL cells (hierarchical fit), sliced per shard."""
+    import torch
+    import torch.distributed as dist
+
+    from .mcmc import fit
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    cl = lk.cells
+    b = shard_bounds(cell_weights(cl.lengths), world)
+    ids = list(range(int(b[rank]), int(b[rank + 1])))
+    vv = None if v0 is None else [v0[c] for c in ids]
+    fr = fit(lk, cells=ids, v0=vv, **fit_kwargs) if ids else None
+    n_max = int(np.max(cl.lengths))
+    local = pack_results(fr, n_max) if fr is not None else np.zeros((0, 4 + len(_SCALARS) + 4 * n_max))
+    rows = gather_rows(local, group=group, device=device)
+    dev = torch.device(device) if device else torch.device("cpu")
+    t = torch.tensor([fr.elapsed_ms if fr else 0.0, fr.n_evals if fr else 0], dtype=torch.float64, device=dev)
+    mx = t.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return unpack_results(rows, cl, cl.name, int(t[1].item()), float(mx[0].item()))
