@@ -578,6 +578,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(prior, double, n);
   TCI_ALLOC(sigma2, double, n);
   TCI_ALLOC(R, double, n * L2);
+  TCI_ALLOC(Rf, float, n * (L * (L + 1) / 2));
   TCI_ALLOC(cov, double, n * L2);
   TCI_ALLOC(work, double, n * L2);
   TCI_ALLOC(cmean, double, n * L);

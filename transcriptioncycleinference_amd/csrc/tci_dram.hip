@@ -81,7 +81,9 @@ __device__ __forceinline__ double2 normal_pair(uint64_t seed, int64_t c, int64_t
   const uint4 r = rng(seed, c, step, purpose, (uint32_t)pair);
   const double u1 = u01(r.x, r.y), u2 = u01(r.z, r.w);
   const double rad = sqrt(-2.0 * log(u1));
-  return make_double2(rad * cos(2.0 * M_PI * u2), rad * sin(2.0 * M_PI * u2));
+  double sn, cs;
+  sincospi(2.0 * u2, &sn, &cs);  // one reduction for both, exact in units of pi
+  return make_double2(rad * cs, rad * sn);
 }
 
 // z[0..P) of stream `purpose` into LDS, one Box-Muller pair per thread and round.
@@ -186,53 +188,87 @@ __device__ double prior_ss(const double* th, const double* mu, const double* sig
 // Proposal factor entries are kept float-representable (see the header).
 __device__ __forceinline__ double f32_round(double x) { return (double)(float)x; }
 
-// Packed upper triangle (row i at i*P - i*(i-1)/2) of a chain's R as fp32 in LDS.
+// Packed upper triangle (row i at i*P - i*(i-1)/2) of a chain's R as fp32: st.Rf holds it in
+// global memory (chain c at c * tri_stride(ld)), written beside every write of R (store_R), so a
+// workgroup stages it into LDS with one coalesced copy.
 __device__ __forceinline__ int tri_off(int i, int P) { return i * P - (i * (i - 1)) / 2; }
-__device__ void load_R_f32(float* Rl, const double* R, int64_t ld, int P) {
-  for (int i = 0; i < P; ++i) {
-    const int oi = tri_off(i, P);
-    for (int j = i + (int)threadIdx.x; j < P; j += kThreads) Rl[oi + j - i] = (float)R[(int64_t)i * ld + j];
-  }
+__host__ __device__ inline int64_t tri_stride(int64_t ld) { return ld * (ld + 1) / 2; }
+__device__ __forceinline__ void store_R(const DramState& st, int64_t c, int P, int i, int j, double v) {
+  st.R[c * st.ld * st.ld + (int64_t)i * st.ld + j] = v;
+  if (j >= i) st.Rf[c * tri_stride(st.ld) + tri_off(i, P) + j - i] = (float)v;
+}
+__device__ void load_R_f32(float* Rl, const DramState& st, int64_t c, int P) {
+  const float* src = st.Rf + c * tri_stride(st.ld);
+  const int tri = P * (P + 1) / 2;
+#pragma unroll 4
+  for (int e = threadIdx.x; e < tri; e += kThreads) Rl[e] = src[e];
 }
 
-// Proposal products U[r][j] = sum_{i<=j} Z[r][i] R[i][j] for r < M <= 16 rows of normals (LDS,
-// row stride zs) and the chain's packed fp32 R (LDS), written to U (LDS, row stride us). One
-// v_mfma_f64_16x16x4_f64 per 4-row k-step of a 16-column tile: A = Z[row = lane&15][k = lane>>4],
-// B = R[k = lane>>4][col = lane&15], D row = (lane>>4) + 4 r, col = lane&15 (cdna_hip_programming.md
-// f64 MFMA map). Tiles skip the k-steps below the triangle; a row's result depends only on that row
-// and the fixed k order, so the fused engine (8 rows: 4 steps x 2 stages) and the per-stage kernels
-// (1 row) produce identical bits. Column tiles go to the 4 waves in snake order (balanced costs).
+// Proposal products U[r][j] = sum_{i<=j} Z[r][i] R[i][j] for r < M <= 16*MT rows of normals (LDS,
+// row stride zs) and the chain's packed fp32 R (LDS); store(r, j, value) receives every product.
+// One v_mfma_f64_16x16x4_f64 per 4-row k-step of a 16 x 16 (row tile, column tile) block:
+// A = Z[row = lane&15][k = lane>>4], B = R[k = lane>>4][col = lane&15], D row = (lane>>4) + 4 q,
+// col = lane&15 (cdna_hip_programming.md f64 MFMA map). Column tiles go to the 4 waves in snake order
+// (balanced triangle costs); a wave runs its (up to CT) column tiles x MT row tiles together, so one
+// A and one B fragment load feed CT*MT independent MFMA chains. Each tile skips the k-steps below
+// the triangle. A product depends only on its row of Z and the fixed k order, so every MT/CT
+// instance (the batched engine's 1-row proposals, the fused engine's 32-row draws) gives the same
+// bits.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-__device__ void mfma_zr(const double* Z, int zs, int M, const float* Rl, int P, double* U, int us) {
+template <int MT, int CT, class Store>
+__device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const float* Rl, int P, Store store) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int row = lane & 15, kq = lane >> 4;
   const int ntiles = (P + 15) >> 4;
-  const int zr = (row < M ? row : M - 1) * zs;  // clamped: rows >= M read row M-1, zeroed below
-  for (int g = 0; 4 * g < ntiles; ++g) {
-    const int nt = 4 * g + ((g & 1) ? 3 - w : w);  // uniform
-    if (nt >= ntiles) continue;
-    const int j = 16 * nt + row;
-    const int jc = j < P ? j : P - 1;
-    const int kmax = min(16 * nt + 15, P - 1);  // uniform: the last row reaching this tile
-    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
-    for (int i0 = 0; i0 <= kmax; i0 += 4) {
-      const int i = i0 + kq;
-      const int ic = i < P ? i : P - 1;
-      const double zv = Z[zr + ic];
-      const float rv = Rl[tri_off(ic, P) + (jc >= ic ? jc - ic : 0)];
-      const double a = (row < M && i < P) ? zv : 0.0;
-      const double b = (i <= j && j < P) ? (double)rv : 0.0;
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  int nt[CT], kmx[CT];
+  int kend = -1;
+#pragma unroll
+  for (int g = 0; g < CT; ++g) {
+    nt[g] = 4 * g + ((g & 1) ? 3 - w : w);  // uniform
+    kmx[g] = nt[g] < ntiles ? min(16 * nt[g] + 15, P - 1) : -1;
+    kend = max(kend, kmx[g]);
+  }
+  f64x4 acc[CT][MT];
+#pragma unroll
+  for (int g = 0; g < CT; ++g)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[g][m] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int i0 = 0; i0 <= kend; i0 += 4) {
+    const int i = i0 + kq;
+    const int ic = i < P ? i : P - 1;
+    double a[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int r = 16 * m + row;
+      const double zv = Z[(r < M ? r : M - 1) * zs + ic];  // clamped: rows >= M read row M-1, zeroed
+      a[m] = (r < M && i < P) ? zv : 0.0;
     }
-    if (j < P) {
-      if (kq < M) U[kq * us + j] = acc[0];
-      if (kq + 4 < M) U[(kq + 4) * us + j] = acc[1];
-      if (kq + 8 < M) U[(kq + 8) * us + j] = acc[2];
-      if (kq + 12 < M) U[(kq + 12) * us + j] = acc[3];
+    const int toff = tri_off(ic, P) - ic;
+#pragma unroll
+    for (int g = 0; g < CT; ++g) {
+      if (i0 > kmx[g]) continue;  // uniform
+      const int j = 16 * nt[g] + row;
+      const int jc = j < P ? j : P - 1;
+      const float rv = Rl[toff + (jc >= ic ? jc : ic)];
+      const double b = (i <= j && j < P) ? (double)rv : 0.0;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[g][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b, acc[g][m], 0, 0, 0);
     }
   }
-  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < CT; ++g) {
+    const int j = 16 * nt[g] + row;
+    if (kmx[g] < 0 || j >= P) continue;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * m + kq + 4 * q;
+        if (r < M) store(r, j, acc[g][m][q]);
+      }
+  }
 }
+constexpr int kZrCT = 5;  // column tiles per wave: P <= 320 (the per-stage kernels' LDS allows P <= 281)
 
 // Dynamic LDS of the per-stage kernels (vector stride L = ld >= P): z, y, red and the chain's R
 // as packed fp32.
@@ -284,9 +320,12 @@ __device__ bool propose_block(const DramState& st, const DramParams& p, int64_t 
                               const double* base, double scale, int P, double* out, Smem& sm) {
   const int64_t ld = st.ld;
   draw_normals(p.seed, st.key[c], step, purpose, P, sm.z, threadIdx.x);
-  load_R_f32(sm.Rl, st.R + c * ld * ld, ld, P);
+  load_R_f32(sm.Rl, st, c, P);
   __syncthreads();
-  mfma_zr(sm.z, sm.L, 1, sm.Rl, P, sm.y, sm.L);
+  double* U = sm.y;
+  const int us = sm.L;
+  mfma_zr<1, kZrCT>(sm.z, sm.L, 1, sm.Rl, P, [=](int r, int j, double v) { U[r * us + j] = v; });
+  __syncthreads();
   int inb = 1;
   for (int j = threadIdx.x; j < P; j += kThreads) {
     const double v = base[j] + scale * sm.y[j];
@@ -310,9 +349,10 @@ __global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* _
     R[e] = 0.0;
     cv[e] = 0.0;
   }
+  for (int64_t e = threadIdx.x; e < tri_stride(ld); e += kThreads) st.Rf[c * tri_stride(ld) + e] = 0.0f;
   __syncthreads();
   for (int j = threadIdx.x; j < P; j += kThreads) {
-    R[(int64_t)j * ld + j] = f32_round(sqrt(qdiag[c * ld + j]));  // R = chol(qcov), qcov = J0 diagonal (:230)
+    store_R(st, c, P, j, j, f32_round(sqrt(qdiag[c * ld + j])));  // R = chol(qcov), qcov = J0 diagonal (:230)
     st.cmean[c * ld + j] = 0.0;
   }
   const double pr = prior_ss(st.theta + c * ld, st.pmu + c * ld, st.psig + c * ld, P, red);
@@ -565,7 +605,7 @@ __global__ __launch_bounds__(kThreads) void k_adapt(DramState st, DramParams p) 
     if (s != 1.0) {
       for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
         const int i = (int)(e / P), j = (int)(e % P);
-        R[(int64_t)i * ld + j] = f32_round(R[(int64_t)i * ld + j] * s);
+        store_R(st, c, P, i, j, f32_round(R[(int64_t)i * ld + j] * s));
       }
     }
     __syncthreads();
@@ -598,7 +638,7 @@ __global__ __launch_bounds__(kThreads) void k_adapt(DramState st, DramParams p) 
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
     for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
       const int i = (int)(e / P), j = (int)(e % P);
-      R[(int64_t)i * ld + j] = j >= i ? f32_round(A[(int64_t)i * lda + j] * sc) : 0.0;
+      store_R(st, c, P, i, j, j >= i ? f32_round(A[(int64_t)i * lda + j] * sc) : 0.0);
     }
   }
   __syncthreads();
@@ -640,14 +680,18 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
   }
 }
 
-constexpr int kDrawSteps = 8;  // steps per MFMA row tile (2 rows per step: 16 rows)
-constexpr int kDrawTiles = 4;  // row tiles per k_draws workgroup (32 steps)
+#ifndef TCI_DRAWS_ABLATE
+#define TCI_DRAWS_ABLATE 0  // diagnostics only (wrong results): bit0 no normals, bit1 no MFMA, bit2 no scalars, bit3 no R load
+#endif
+constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each)
+constexpr int kDrawSteps = 8 * kDrawMT;   // steps per pass (2 rows per step)
+constexpr int kDrawPasses = 2;            // passes per k_draws workgroup (32 steps)
 enum DrawSlot { D_Q21 = 0, D_Q01 = 1, D_U1 = 2, D_U2 = 3, D_G = 4 };
 
-// Dynamic LDS of k_draws: the tile's normals and products (2 x 16 rows of stride L) and the chain's
-// R as packed fp32.
+// Dynamic LDS of k_draws: one pass's normals (2 x kDrawSteps rows of stride L) and the chain's R
+// as packed fp32.
 __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
-  return (2 * 2 * kDrawSteps * L) * 8 + (L * (L + 1) / 2) * 4 + 16;
+  return (2 * kDrawSteps * L) * 8 + (L * (L + 1) / 2) * 4 + 16;
 }
 
 __global__ __launch_bounds__(kThreads) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end) {
@@ -661,37 +705,39 @@ __global__ __launch_bounds__(kThreads) void k_draws(DramState st, DramParams p, 
   const int64_t DW = draw_stride(ld);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   double* Z = dyn;
-  double* U = Z + 2 * kDrawSteps * L;
-  float* Rl = reinterpret_cast<float*>(U + 2 * kDrawSteps * L);
-  load_R_f32(Rl, st.R + c * ld * ld, ld, P);
+  float* Rl = reinterpret_cast<float*>(Z + 2 * kDrawSteps * L);
+  if (!(TCI_DRAWS_ABLATE & 8)) load_R_f32(Rl, st, c, P);
   const double a = 0.5 * (double)st.nobs[c];
   const double inv_ds = 1.0 / p.drscale;
-  for (int tile = 0; tile < kDrawTiles; ++tile) {
-    const int64_t step0 = s_begin + ((int64_t)blockIdx.y * kDrawTiles + tile) * kDrawSteps;
+  double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
+  for (int pass = 0; pass < kDrawPasses; ++pass) {
+    const int64_t step0 = s_begin + ((int64_t)blockIdx.y * kDrawPasses + pass) * kDrawSteps;
     if (step0 > s_end) break;  // uniform over the workgroup
     const int ns = (int)min<int64_t>(kDrawSteps, s_end - step0 + 1);
-    draw_block_normals(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
-    __syncthreads();  // (the first tile: also R)
-    mfma_zr(Z, L, 2 * ns, Rl, P, U, L);
-    double* d0 = st.draws + (c * p.chunk + (step0 - s_begin)) * DW;
-    for (int k = 0; k < ns; ++k)
-      for (int j = threadIdx.x; j < P; j += kThreads) {
-        d0[k * DW + j] = U[2 * k * L + j];
-        d0[k * DW + ld + j] = U[(2 * k + 1) * L + j];
-      }
+    if (!(TCI_DRAWS_ABLATE & 1)) draw_block_normals(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
+    __syncthreads();  // (the first pass: also R)
+    // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
+    double* d0 = drow + step0 * DW;
+    if (!(TCI_DRAWS_ABLATE & 2))
+      mfma_zr<kDrawMT, kZrCT>(Z, L, 2 * ns, Rl, P,
+                              [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; });
     for (int k = w; k < ns; k += kThreads / 64) {
-      const int64_t step = step0 + k;
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
       if (lane == 0) {
         double* sc = d0 + k * DW + 2 * ld;
         sc[D_Q21] = q.x;
         sc[D_Q01] = q.y;
-        sc[D_U1] = uniform_at(p.seed, key, step, P_U1);
-        sc[D_U2] = uniform_at(p.seed, key, step, P_U2);
-        sc[D_G] = p.updatesigma ? gamma_unit(p.seed, key, step, a) : 1.0;
       }
     }
-    __syncthreads();  // Z and U are rewritten by the next tile
+    __syncthreads();  // Z is rewritten by the next pass
+  }
+  // the scalar draws of the workgroup's steps, one step per thread
+  const int64_t step = s_begin + (int64_t)blockIdx.y * kDrawPasses * kDrawSteps + threadIdx.x;
+  if (!(TCI_DRAWS_ABLATE & 4) && threadIdx.x < kDrawPasses * kDrawSteps && step <= s_end) {
+    double* sc = drow + step * DW + 2 * ld;
+    sc[D_U1] = uniform_at(p.seed, key, step, P_U1);
+    sc[D_U2] = uniform_at(p.seed, key, step, P_U2);
+    sc[D_G] = p.updatesigma ? gamma_unit(p.seed, key, step, a) : 1.0;
   }
 }
 
@@ -949,7 +995,7 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
   if (lds > 48 * 1024 &&
       hipFuncSetAttribute((const void*)k_draws, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return TCI_EHIP;
-  const int64_t per_wg = (int64_t)kDrawSteps * kDrawTiles;
+  const int64_t per_wg = (int64_t)kDrawSteps * kDrawPasses;
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
   hipLaunchKernelGGL(k_draws, dim3((unsigned)st.n_chains, gy), dim3(kThreads), lds, stream, st, p, s_begin, s_end);
   hipLaunchKernelGGL((k_chain<RPL, NSEG>), dim3((unsigned)st.n_chains), dim3(kThreads), 0, stream, st, p, kp,
@@ -980,6 +1026,9 @@ int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, 
 //     packed LDS triangle when it becomes the panel, wave 0 eliminates inside the panel, every
 //     owner applies the rank-4 update to its later tiles in registers (2 barriers per panel).
 //     R rows are the panel rows scaled by adascale / sqrt(pivot).
+#ifndef TCI_ADAPT_ABLATE
+#define TCI_ADAPT_ABLATE 0  // diagnostics only (wrong results): bit0 skip the Cholesky, bit1 skip the covupd passes
+#endif
 constexpr int kAdaptTiles = 3;  // tiles per thread: NT(NT+1)/2 <= 768, NT = ceil(P/4)
 __host__ __device__ inline int adapt_ls(int P) { return (P + 3) & ~3; }
 __host__ __device__ inline int64_t adapt_tiles_lds_bytes(int64_t P) {
@@ -1025,8 +1074,8 @@ __global__ __launch_bounds__(kThreads) void k_adapt_tiles(DramState st, DramPara
       }
     }
   }
-  const int nb = (int)p.adaptint;
-  const int rb = max(1, min(nb, tri / Ls));  // rows per LDS batch
+  const int nb = (TCI_ADAPT_ABLATE & 2) ? 0 : (int)p.adaptint;
+  const int rb = max(1, min((int)p.adaptint, tri / Ls));  // rows per LDS batch
   const double* win = st.window + c * p.adaptint * ld;
   // ---- pass 1: batch mean (row order fixed: deterministic)
   double s0 = 0.0, s1 = 0.0;
@@ -1127,7 +1176,7 @@ __global__ __launch_bounds__(kThreads) void k_adapt_tiles(DramState st, DramPara
     if (s != 1.0) {
       for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
         const int i = (int)(e / P), j = (int)(e % P);
-        R[(int64_t)i * ld + j] = f32_round(R[(int64_t)i * ld + j] * s);
+        store_R(st, c, P, i, j, f32_round(R[(int64_t)i * ld + j] * s));
       }
     }
     __syncthreads();
@@ -1137,7 +1186,7 @@ __global__ __launch_bounds__(kThreads) void k_adapt_tiles(DramState st, DramPara
   // ---- blocked LDL' of cov + qcovadj I on the packed triangle
   if (t == 0) fail = 0;
   __syncthreads();
-  for (int pp = 0; pp < NT; ++pp) {
+  for (int pp = 0; pp < ((TCI_ADAPT_ABLATE & 1) ? 0 : NT); ++pp) {
 #pragma unroll
     for (int k = 0; k < kAdaptTiles; ++k) {
       if (ti_[k] != pp) continue;
@@ -1190,12 +1239,12 @@ __global__ __launch_bounds__(kThreads) void k_adapt_tiles(DramState st, DramPara
     }
   }
   __syncthreads();
-  if (!fail) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
+  if (!fail && !(TCI_ADAPT_ABLATE & 1)) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
     for (int i = 0; i < P; ++i) {
       const int oi = off(i);
       const double di = sqrt(A[oi]);
-      for (int j = i + t; j < P; j += kThreads) R[(int64_t)i * ld + j] = f32_round(A[oi + j - i] / di * sc);
+      for (int j = i + t; j < P; j += kThreads) store_R(st, c, P, i, j, f32_round(A[oi + j - i] / di * sc));
     }
   }
   __syncthreads();

@@ -26,6 +26,7 @@ struct DramState {
   double* prior;           // prior SS of the current state
   double* sigma2;          // error variance (model.sigma2, :259)
   double* R;               // proposal Cholesky factor (upper, float-representable): proposal = theta + z * R
+  float* Rf;               // the same R as packed fp32 upper triangles (chain c at c * ld(ld+1)/2)
   double* cov;             // running chain covariance / mean / weight (mcmcstat covupd)
   double* cmean;
   double* wsum;
