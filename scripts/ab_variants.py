@@ -25,6 +25,7 @@ VARIANTS = {
     "w8_latepts": ["TCI_WAVES_PER_EU=8", "TCI_EARLY_POINTS=0"],
     "loopramp": ["TCI_RAMP_PREFIX=0"],
     "abl_loads": ["TCI_ABLATE=16"],
+    "chainprof": ["TCI_CHAIN_PROFILE=1"],
     "adapt_nochol": ["TCI_ADAPT_ABLATE=1"],
     "adapt_nocov": ["TCI_ADAPT_ABLATE=2"],
     "draws_nonorm": ["TCI_DRAWS_ABLATE=1"],

@@ -602,6 +602,10 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(sq_mean, double, n);
   TCI_ALLOC(sq_m2, double, n);
   TCI_ALLOC(step, int64_t, 1);
+#ifdef TCI_CHAIN_PROFILE
+  TCI_ALLOC(prof, int64_t, 8);
+  TCI_HIP(ctx, hipMemsetAsync(st.prof, 0, 8 * sizeof(int64_t), ctx->stream));
+#endif
   if (n_keep > 0 && (out->chain || out->s2chain)) {
     TCI_ALLOC(chain_out, double, (size_t)n_keep * n * L);
     TCI_ALLOC(s2_out, double, (size_t)n_keep * n);
@@ -719,6 +723,15 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_HIP(ctx, hipStreamSynchronize(s));
   if (exec) (void)hipGraphExecDestroy(exec);
   if (graph) (void)hipGraphDestroy(graph);
+#ifdef TCI_CHAIN_PROFILE
+  {
+    int64_t ph[8];
+    TCI_HIP(ctx, hipMemcpy(ph, st.prof, sizeof(ph), hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "{\"k_chain_cycles_per_chain\": [");
+    for (int k = 0; k < 8; ++k) std::fprintf(stderr, "%s%.1f", k ? ", " : "", (double)ph[k] / (double)n);
+    std::fprintf(stderr, "]}\n");
+  }
+#endif
   if (ge != hipSuccess) return hip_fail(ctx, ge, "DRAM step replay");
   if (rc != TCI_OK) return fail(ctx, rc, "DRAM step launch");
   float ms = 0.f;

@@ -126,10 +126,15 @@ __device__ __forceinline__ double gamma_at(uint64_t seed, int64_t c, int64_t ste
   return gamma_unit(seed, c, step, a) * scale;
 }
 
-__device__ __forceinline__ double wsum64(double x) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
-  return x;
+// Wave sum, result in every lane: DPP inclusive scan + lane 63 (tci_eval.h), no LDS round trips.
+// Every engine reduces through this one function, so their bits agree.
+__device__ __forceinline__ double wsum64(double x) { return lane63(wave_incl_scan(x)); }
+
+// Lane l's value of x in every lane (readlane: scalar broadcast, l uniform).
+__device__ __forceinline__ double lane_bcast(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
 }
 
 constexpr int kVec = TCI_MAX_POINTS + 8;
@@ -686,7 +691,7 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
 constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each)
 constexpr int kDrawSteps = 8 * kDrawMT;   // steps per pass (2 rows per step)
 constexpr int kDrawPasses = 2;            // passes per k_draws workgroup (32 steps)
-enum DrawSlot { D_Q21 = 0, D_Q01 = 1, D_U1 = 2, D_U2 = 3, D_G = 4 };
+enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
 
 // Dynamic LDS of k_draws: one pass's normals (2 x kDrawSteps rows of stride L) and the chain's R
 // as packed fp32.
@@ -723,11 +728,7 @@ __global__ __launch_bounds__(kThreads) void k_draws(DramState st, DramParams p, 
                               [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; });
     for (int k = w; k < ns; k += kThreads / 64) {
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
-      if (lane == 0) {
-        double* sc = d0 + k * DW + 2 * ld;
-        sc[D_Q21] = q.x;
-        sc[D_Q01] = q.y;
-      }
+      if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
     }
     __syncthreads();  // Z is rewritten by the next pass
   }
@@ -739,29 +740,6 @@ __global__ __launch_bounds__(kThreads) void k_draws(DramState st, DramParams p, 
     sc[D_U2] = uniform_at(p.seed, key, step, P_U2);
     sc[D_G] = p.updatesigma ? gamma_unit(p.seed, key, step, a) : 1.0;
   }
-}
-
-// One chain row's draws (this lane's vector entries j = lane + 64 k and the scalars).
-template <int NJ>
-struct StepDraws {
-  double u1[NJ], u2[NJ];
-  double q21, q01, U1, U2, G;
-};
-template <int NJ>
-__device__ __forceinline__ void load_draws(StepDraws<NJ>& d, const double* __restrict__ src, int64_t ld, int P,
-                                           int lane) {
-#pragma unroll
-  for (int k = 0; k < NJ; ++k) {
-    const int j = lane + 64 * k;
-    d.u1[k] = j < P ? src[j] : 0.0;
-    d.u2[k] = j < P ? src[ld + j] : 0.0;
-  }
-  const double* sc = src + 2 * ld;
-  d.q21 = sc[D_Q21];
-  d.q01 = sc[D_Q01];
-  d.U1 = sc[D_U1];
-  d.U2 = sc[D_U2];
-  d.G = sc[D_G];
 }
 
 // wave_prior on register-held vectors (entry k of lane l is j = l + 64 k): the same per-lane
@@ -779,13 +757,34 @@ __device__ __forceinline__ double wave_prior_reg(const double* y, const double* 
   return wsum64(s);
 }
 
-// record_vec on register-held vectors by one wave (smn/sm2: this lane's Welford entries).
+// Where chain row `row` goes, advanced row by row without 64-bit divisions on the step path:
+// its covupd window slot (row - 1) % adaptint and, when (row - 1) % thin == 0, its output row.
+struct RowCursor {
+  int64_t win, tpos, keep;  // window slot; (row - 1) % thin; (row - 1) / thin
+  __device__ void init(const DramParams& p, int64_t row) {
+    win = p.adaptint > 0 ? (row - 1) % p.adaptint : 0;
+    tpos = p.thin > 0 ? (row - 1) % p.thin : 1;
+    keep = p.thin > 0 ? (row - 1) / p.thin : 0;
+  }
+  __device__ void next(const DramParams& p) {
+    if (++win == p.adaptint) win = 0;
+    if (p.thin > 0 && ++tpos == p.thin) {
+      tpos = 0;
+      ++keep;
+    }
+  }
+  __device__ bool kept(const DramParams& p) const { return p.thin > 0 && tpos == 0 && keep < p.n_keep; }
+};
+
+// record_vec on register-held vectors by one wave (smn/sm2: this lane's Welford entries): the same
+// stores and Welford arithmetic as record_vec.
 template <int NJ>
 __device__ __forceinline__ void record_vec_reg(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P,
-                                               const double* th, double* smn, double* sm2, int lane) {
+                                               const double* th, double* smn, double* sm2, int lane,
+                                               const RowCursor& cur) {
   const int64_t ld = st.ld;
   if (p.adaptint > 0) {
-    double* w = st.window + (c * p.adaptint + (row - 1) % p.adaptint) * ld;
+    double* w = st.window + (c * p.adaptint + cur.win) * ld;
 #pragma unroll
     for (int k = 0; k < NJ; ++k)
       if (lane + 64 * k < P) w[lane + 64 * k] = th[k];
@@ -804,30 +803,65 @@ __device__ __forceinline__ void record_vec_reg(const DramState& st, const DramPa
       }
     }
   }
-  if (st.chain_out != nullptr && p.thin > 0 && (row - 1) % p.thin == 0) {
-    const int64_t kk = (row - 1) / p.thin;
-    if (kk < p.n_keep)
+  if (st.chain_out != nullptr && cur.kept(p))
 #pragma unroll
-      for (int k = 0; k < NJ; ++k)
-        if (lane + 64 * k < P) st.chain_out[(kk * st.n_chains + c) * ld + lane + 64 * k] = th[k];
-  }
+    for (int k = 0; k < NJ; ++k)
+      if (lane + 64 * k < P) st.chain_out[(cur.keep * st.n_chains + c) * ld + lane + 64 * k] = th[k];
+}
+
+// record_s2 with the row's place from the cursor.
+__device__ __forceinline__ void record_s2_cur(const DramState& st, const DramParams& p, int64_t c, int64_t row,
+                                              double s2, S2Stats& a, const RowCursor& cur) {
+  a.sum += s2;
+  const double q = sqrt(s2), n = (double)row;
+  const double d = q - a.qmean;
+  a.qmean += d / n;
+  a.qm2 += d * (q - a.qmean);
+  if (st.s2_out != nullptr && cur.kept(p)) st.s2_out[cur.keep * st.n_chains + c] = s2;
+}
+
+#ifndef TCI_CHAIN_PROFILE
+#define TCI_CHAIN_PROFILE 0  // diagnostics: s_memtime cycles per k_chain phase (wave 0) into st.prof
+#endif
+__device__ __forceinline__ uint64_t stamp() {
+#if TCI_CHAIN_PROFILE
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+#else
+  return 0;
+#endif
 }
 
 template <int RPL, int NSEG>
 __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
                                                     int64_t s_end) {
+  // Round structure (one workgroup barrier per round). At the start of a round the state after
+  // row s-1 is known. Wave w evaluates proposal (stage w&1) of step s + (w>>1): waves 0/1 the
+  // stage-1/2 proposals of step s, waves 2/3 those of step s+1 drawn around the SAME state, i.e.
+  // speculating that step s does not move the chain (the common case: mcmcstat's DRAM accepts a
+  // minority of steps). After the barrier every wave takes step s's decisions; when the chain did
+  // not move, step s+1's evaluations are exactly the ones the sequential sampler would make, and
+  // step s+1 is decided in the same round. Decisions, counters and records are those of the
+  // step-by-step sampler (and of the batched engine) bit for bit.
   constexpr int NJ = RPL + 1;  // vector entries per lane: P = 7 + N <= 64 RPL + 8 <= 64 NJ
   constexpr int EV = eval_lds_doubles<RPL>();
-  __shared__ __attribute__((aligned(16))) double evl[2][EV];  // the two evaluating waves' tables
-  __shared__ double yl[2][64 * NJ];                            // the proposal each of them evaluates
-  __shared__ double xch[2][4];  // by step parity: ss1, ss2, prior1, prior2
+  constexpr int NW = kThreads / 64;
+  __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each evaluating wave's tables
+  __shared__ double yl[2][NW][64 * NJ];                         // by round parity: each wave's proposal
+  __shared__ double xch[2][NW][4];                              // by round parity: ss, prior, in-bounds of each
+  __shared__ double xsc[2][2][5];                               // by round parity: scalar draws of s, s+1
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int64_t DW = draw_stride(ld);
-  const double* drow = st.draws + c * p.chunk * DW - s_begin * DW;  // row of step s: drow + s * DW
+  const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
+  const int stage = w & 1, ahead = w >> 1;                        // this wave's proposal
+  const double scale = stage ? 1.0 / p.drscale : 1.0;
   double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], smn[NJ], sm2[NJ];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
@@ -836,17 +870,16 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     th[k] = in ? st.theta[c * ld + j] : 0.0;
     lo[k] = in ? st.lower[c * ld + j] : 0.0;
     hi[k] = in ? st.upper[c * ld + j] : 0.0;
-    mu[k] = sg[k] = smn[k] = sm2[k] = 0.0;
-    if (w == 2 && in) {
-      mu[k] = st.pmu[c * ld + j];
-      sg[k] = st.psig[c * ld + j];
+    mu[k] = in ? st.pmu[c * ld + j] : 0.0;
+    sg[k] = in ? st.psig[c * ld + j] : 0.0;
+    smn[k] = sm2[k] = 0.0;
+    if (w == 0 && in) {  // wave 0 keeps the posterior Welford statistics
       smn[k] = st.smean[c * ld + j];
       sm2[k] = st.sm2[c * ld + j];
     }
   }
-  // the chain's cell records stay in the registers of the two evaluating waves
-  EvalIn<RPL> e;
-  if (w < 2) {
+  EvalIn<RPL> e;  // the chain's cell records stay in registers
+  {
     const int cell = st.cell[c];
     const int64_t cbase = (int64_t)cell * kp.cell_stride;
     e.cm = kp.cells[cell];
@@ -859,123 +892,178 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     }
   }
   double ss = st.ss[c], prior = st.prior[c], s2 = st.sigma2[c];
-  S2Stats s2a{0.0, 0.0, 0.0};  // held by wave 3
-  if (w == 3) s2a = S2Stats{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
+  S2Stats s2a{0.0, 0.0, 0.0};  // held by wave 1
+  if (w == 1) s2a = S2Stats{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
   int32_t nacc = st.naccept[c], nrej = st.nrej_win[c];
   int64_t nev = st.nevals[c];
-  const double scale2 = 1.0 / p.drscale;
-  StepDraws<NJ> d;
-  load_draws<NJ>(d, drow + s_begin * DW, ld, P, lane);
-  for (int64_t step = s_begin; step <= s_end; ++step) {
-    const int par = (int)(step & 1);
-    StepDraws<NJ> dn;  // the next row's draws, in flight during this step
-    load_draws<NJ>(dn, drow + (step < s_end ? step + 1 : step) * DW, ld, P, lane);
-    // ---- proposals: stage 1 theta + z1*R, stage 2 theta + z2*R/drscale; bounds by wave vote
-    double y1[NJ], y2[NJ];
-    bool out1 = false, out2 = false;
+  // this wave's proposal offsets: rows s + ahead (cur), s + ahead + 1, s + ahead + 2 (prefetched)
+  auto load_u = [&](double* u, int64_t row) {
+    const double* src = drow + min(row, s_end) * DW + stage * ld;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) u[k] = lane + 64 * k < P ? src[lane + 64 * k] : 0.0;
+  };
+  double ucur[NJ], un1[NJ], un2[NJ];
+  load_u(ucur, s_begin + ahead);
+  load_u(un1, s_begin + ahead + 1);
+  load_u(un2, s_begin + ahead + 2);
+  int par = 0;
+  RowCursor cur;
+  cur.init(p, s_begin);
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0}, t0 = stamp(), t1;
+#define TCI_PHASE(k) \
+  if (TCI_CHAIN_PROFILE) { t1 = stamp(); ph[k] += t1 - t0; t0 = t1; }
+  for (int64_t s = s_begin; s <= s_end; par ^= 1) {
+    const bool has_next = s + 1 <= s_end;
+    // wave 3 fetches the scalar draws of steps s, s+1 (lanes 0-9) while it evaluates
+    double scv = 0.0;
+    if (w == NW - 1 && lane < 10) scv = drow[min(s + lane / 5, s_end) * DW + 2 * ld + lane % 5];
+    // ---- this wave's proposal and its bounds (wave vote)
+    double y[NJ];
+    bool out = false;
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
-      y1[k] = th[k] + 1.0 * d.u1[k];
-      y2[k] = th[k] + scale2 * d.u2[k];
-      if (lane + 64 * k < P) {
-        out1 |= !(y1[k] >= lo[k] && y1[k] <= hi[k]);
-        out2 |= !(y2[k] >= lo[k] && y2[k] <= hi[k]);
-      }
+      y[k] = th[k] + scale * ucur[k];
+      if (lane + 64 * k < P) out |= !(y[k] >= lo[k] && y[k] <= hi[k]);
     }
-    const bool inb1 = wave_ballot(out1) == 0;
-    const bool inb2 = wave_ballot(out2) == 0 && p.ntry >= 2;
-    // ---- ssfun at both proposals (waves 0, 1; out of bounds: not called, +Inf), the priors and
-    //      the previous row's record (wave 2), the previous row's sigma2 record (wave 3)
-    if (w < 2) {
-      double r = INFINITY;
-      if (w == 0 ? inb1 : inb2) {
-        double* yb = yl[w];
+    const bool active = (stage == 0 || p.ntry >= 2) && (ahead == 0 || has_next);
+    const bool inb = active && wave_ballot(out) == 0;
+    double r = INFINITY, pr = 0.0;
+    TCI_PHASE(0)
+    if (inb) {
+      double* yb = yl[par][w];
 #pragma unroll
-        for (int k = 0; k < NJ; ++k) yb[lane + 64 * k] = w == 0 ? y1[k] : y2[k];
-        wave_sync();
-        e.v = yb[0];
-        e.tau = yb[1];
-        e.ton = yb[2];
-        e.b1 = yb[3];
-        e.b2 = yb[4];
-        e.A = yb[5];
-        e.R = yb[6];
+      for (int k = 0; k < NJ; ++k) yb[lane + 64 * k] = y[k];
+      wave_sync();
+      e.v = yb[0];
+      e.tau = yb[1];
+      e.ton = yb[2];
+      e.b1 = yb[3];
+      e.b2 = yb[4];
+      e.A = yb[5];
+      e.R = yb[6];
 #pragma unroll
-        for (int q = 0; q < RPL; ++q) {
-          const int g = RPL * lane + q;
-          e.dr[q] = 7 + g < P ? yb[7 + g] : 0.0;
-        }
-        r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
+      for (int q = 0; q < RPL; ++q) {
+        const int g = RPL * lane + q;
+        e.dr[q] = 7 + g < P ? yb[7 + g] : 0.0;
       }
-      if (lane == 0) xch[par][w] = r;
-    } else if (w == 2) {
-      const double pr1 = inb1 ? wave_prior_reg<NJ>(y1, mu, sg, P, lane) : 0.0;
-      const double pr2 = inb2 ? wave_prior_reg<NJ>(y2, mu, sg, P, lane) : 0.0;
-      if (lane == 0) {
-        xch[par][2] = pr1;
-        xch[par][3] = pr2;
-      }
-      if (step > s_begin) record_vec_reg<NJ>(st, p, c, step - 1, P, th, smn, sm2, lane);
-    } else if (step > s_begin && lane == 0) {
-      record_s2(st, p, c, step - 1, s2, s2a);
+      r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
+      TCI_PHASE(1)
+      pr = wave_prior_reg<NJ>(y, mu, sg, P, lane);
     }
+    TCI_PHASE(2)
+    if (lane == 0) {
+      xch[par][w][0] = r;
+      xch[par][w][1] = pr;
+      xch[par][w][2] = inb ? 1.0 : 0.0;
+    }
+    if (w == NW - 1 && lane < 10) xsc[par][lane / 5][lane % 5] = scv;
     __syncthreads();
-    const double ss1 = xch[par][0], ss2 = xch[par][1];
-    // ---- stage 1 (k_accept1)
-    double a12 = 0.0, pr1 = 0.0;
-    bool acc = false;
-    if (inb1) {
-      nev += 1;
-      pr1 = xch[par][2];
-      const double ex = -0.5 * (ss1 - ss) / s2 - 0.5 * (pr1 - prior);
-      a12 = fmin(1.0, exp(ex));
-      acc = d.U1 < a12;
-    }
-    // ---- stage 2 (k_accept2)
-    bool acc2 = false;
-    double pr2 = 0.0;
-    if (!acc && inb2) {
-      nev += 1;
-      pr2 = xch[par][3];
-      const double a32 = fmin(1.0, exp(-0.5 * (ss1 - ss2) / s2 - 0.5 * (pr1 - pr2)));
-      const double l2 = exp(-0.5 * (ss2 - ss) / s2 - 0.5 * (pr2 - prior));
-      const double q1 = exp(-0.5 * (d.q21 - d.q01));
-      const double a13 = l2 * q1 * (1.0 - a32) / (1.0 - a12);
-      acc2 = d.U2 < a13;
-    }
-    if (acc || acc2) {
+    TCI_PHASE(3)
+    // ---- decisions: step s, then (if the chain did not move) step s+1 from the speculation.
+    // Every transcendental/division the two steps can need is evaluated ONCE, in parallel lanes
+    // (the sequential sampler's exact expressions, per-lane operands), then picked by readlane:
+    //   level 1, lanes 0-5: sigma2 after step s (lanes 0-2: state unchanged / stage-1 / stage-2
+    //            move) and after step s+1 with step s unmoved (lanes 3-5): 1 / (G * (2 / SS));
+    //   level 2, lanes 0-2 (step s) and 3-5 (step s+1, sigma2 = lane 0's): a12, a32, l2;
+    //   level 3, lanes 0/1: a13 = l2 q1 (1 - a32) / (1 - a12) of step s / s+1.
+    const double* X0 = xch[par][0];
+    const double* X1 = xch[par][1];
+    const double* X2 = xch[par][2];
+    const double* X3 = xch[par][3];
+    const double* SC0 = xsc[par][0];
+    const double* SC1 = xsc[par][1];
+    const bool inb1a = X0[2] != 0.0, inb2a = X1[2] != 0.0, inb1b = X2[2] != 0.0, inb2b = X3[2] != 0.0;
+    const double pr1a = inb1a ? X0[1] : 0.0, pr2a = inb2a ? X1[1] : 0.0;
+    const double pr1b = inb1b ? X2[1] : 0.0, pr2b = inb2b ? X3[1] : 0.0;
+    const int h = lane < 3 ? 0 : 1, k3 = lane < 3 ? lane : lane - 3;  // lanes >= 6 compute junk
+    const double ssA = h ? X2[0] : X0[0], ssB = h ? X3[0] : X1[0];
+    const double Gh = h ? SC1[D_G] : SC0[D_G];
+    const double s2n = 1.0 / (Gh * (2.0 / (k3 == 0 ? ss : k3 == 1 ? ssA : ssB)));
+    const double s2n0 = lane_bcast(s2n, 0);
+    const double s2u = (h && p.updatesigma) ? s2n0 : s2;  // step s+1 runs at sigma2 after an unmoved step s
+    const double prA = h ? pr1b : pr1a, prB = h ? pr2b : pr2a;
+    // one expression, per-lane operands: a12 (k3 = 0), a32 (k3 = 1), l2 (k3 = 2)
+    const double eA = k3 == 2 ? ssB : ssA, eB = k3 == 1 ? ssB : ss;
+    const double eC = k3 == 2 ? prB : prA, eD = k3 == 1 ? prB : prior;
+    const double ev = exp(-0.5 * (eA - eB) / s2u - 0.5 * (eC - eD));
+    const double av = k3 == 2 ? ev : fmin(1.0, ev);
+    const double a12a = lane_bcast(av, 0), a32a = lane_bcast(av, 1), l2a = lane_bcast(av, 2);
+    const double a12b = lane_bcast(av, 3), a32b = lane_bcast(av, 4), l2b = lane_bcast(av, 5);
+    const double q1h = lane == 0 ? SC0[D_Q1] : SC1[D_Q1];
+    const double l2h = lane == 0 ? l2a : l2b, a32h = lane == 0 ? a32a : a32b, a12h = lane == 0 ? a12a : a12b;
+    const double a13v = l2h * q1h * (1.0 - a32h) / (1.0 - a12h);  // lane 0: step s, lane 1: step s+1
+    const double a13a = lane_bcast(a13v, 0), a13b = lane_bcast(a13v, 1);
+    const double s2_0 = s2n0, s2_1 = lane_bcast(s2n, 1), s2_2 = lane_bcast(s2n, 2);
+    const double s2_3 = lane_bcast(s2n, 3), s2_4 = lane_bcast(s2n, 4), s2_5 = lane_bcast(s2n, 5);
+    int adv = 0;
+    for (int hh = 0; hh < 2; ++hh) {
+      if (hh == 1 && !has_next) break;
+      const double* x1 = hh ? X2 : X0;
+      const double* x2 = hh ? X3 : X1;
+      const double* sc = hh ? SC1 : SC0;
+      const bool inb1 = hh ? inb1b : inb1a, inb2 = hh ? inb2b : inb2a;
+      bool acc = false, acc2 = false;
+      if (inb1) {
+        nev += 1;
+        acc = sc[D_U1] < (hh ? a12b : a12a);
+      }
+      if (!acc && inb2) {
+        nev += 1;
+        acc2 = sc[D_U2] < (hh ? a13b : a13a);
+      }
+      const bool moved = acc || acc2;
+      if (moved) {
+        const double* yb = yl[par][2 * hh + (acc ? 0 : 1)];
 #pragma unroll
-      for (int k = 0; k < NJ; ++k) th[k] = acc ? y1[k] : y2[k];
-      ss = acc ? ss1 : ss2;
-      prior = acc ? pr1 : pr2;
-      nacc += 1;
-    } else {
-      nrej += 1;
+        for (int k = 0; k < NJ; ++k) th[k] = yb[lane + 64 * k];
+        ss = acc ? x1[0] : x2[0];
+        prior = acc ? (hh ? pr1b : pr1a) : (hh ? pr2b : pr2a);
+        nacc += 1;
+      } else {
+        nrej += 1;
+      }
+      // sigma2 Gibbs update of this row (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/ss)
+      if (p.updatesigma) s2 = hh ? (acc ? s2_4 : acc2 ? s2_5 : s2_3) : (acc ? s2_1 : acc2 ? s2_2 : s2_0);
+      // the row's records
+      const int64_t row = s + hh;
+      if (w == 0) record_vec_reg<NJ>(st, p, c, row, P, th, smn, sm2, lane, cur);
+      if (w == 1 && lane == 0) record_s2_cur(st, p, c, row, s2, s2a, cur);
+      cur.next(p);
+      adv = hh + 1;
+      if (moved) break;  // step s+1 must be re-proposed around the new state
     }
-    // sigma2 Gibbs update of this row (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/ss)
-    if (p.updatesigma) s2 = 1.0 / (d.G * (2.0 / ss));
-    d = dn;
+    TCI_PHASE(4)
+    // ---- advance the proposal offsets by adv rows
+    if (adv == 1) {
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) {
+        ucur[k] = un1[k];
+        un1[k] = un2[k];
+      }
+      load_u(un2, s + 1 + ahead + 2);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) ucur[k] = un2[k];
+      load_u(un1, s + 2 + ahead + 1);
+      load_u(un2, s + 2 + ahead + 2);
+    }
+    s += adv;
+    TCI_PHASE(5)
+    if (TCI_CHAIN_PROFILE) ph[5] += 1ull << 40;  // round count in the high bits
   }
-  // the last row of the chunk
-  if (w == 2) {
-    record_vec_reg<NJ>(st, p, c, s_end, P, th, smn, sm2, lane);
+#undef TCI_PHASE
+  if (TCI_CHAIN_PROFILE && w == 0 && lane == 0 && st.prof != nullptr)
+    for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long*)&st.prof[k], (unsigned long long)ph[k]);
+  if (w == 0) {
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
       const int j = lane + 64 * k;
       if (j < P) {
+        st.theta[c * ld + j] = th[k];
         st.smean[c * ld + j] = smn[k];
         st.sm2[c * ld + j] = sm2[k];
       }
     }
-  } else if (w == 3 && lane == 0) {
-    record_s2(st, p, c, s_end, s2, s2a);
-    st.s2sum[c] = s2a.sum;
-    st.sq_mean[c] = s2a.qmean;
-    st.sq_m2[c] = s2a.qm2;
-  } else if (w == 0) {
-#pragma unroll
-    for (int k = 0; k < NJ; ++k)
-      if (lane + 64 * k < P) st.theta[c * ld + lane + 64 * k] = th[k];
     if (lane == 0) {
       st.ss[c] = ss;
       st.prior[c] = prior;
@@ -985,6 +1073,10 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       st.nevals[c] = nev;
       if (c == 0) *st.step = s_end;  // k_adapt reads the row it follows
     }
+  } else if (w == 1 && lane == 0) {
+    st.s2sum[c] = s2a.sum;
+    st.sq_mean[c] = s2a.qmean;
+    st.sq_m2[c] = s2a.qm2;
   }
 }
 
@@ -1311,7 +1403,7 @@ int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& k
   }
 }
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl) {
-  const int64_t chain = 2 * (4 * 64 * rpl + 4 * rpl) * 8 + 2 * 64 * (rpl + 1) * 8 + 64;  // k_chain (static)
+  const int64_t chain = (4 * (4 * 64 * rpl + 4 * rpl) + 2 * 4 * 64 * (rpl + 1) + 2 * 4 * 4 + 2 * 2 * 5) * 8;  // k_chain
   return std::max<int64_t>(chain, draws_lds_bytes(ld));                                  // k_draws (dynamic)
 }
 int dram_launch_step_incr(const DramState& st, void* stream) {

@@ -52,6 +52,7 @@ struct DramState {
   double* s2_out;          // optional thinned s2 rows
   double* work;            // Cholesky workspace (n_chains x ld x ld)
   int64_t* step;           // current chain row (1-based), advanced on device after each step
+  int64_t* prof;           // TCI_CHAIN_PROFILE builds only: k_chain phase cycles, summed over chains
   double* draws;           // fused engine: per chain, p.chunk rows of draw_stride(ld) doubles (k_draws)
 };
 
