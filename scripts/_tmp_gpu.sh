@@ -1,2 +1,3 @@
-bash scripts/gpu_dram_check.sh dr6 || exit 1
-for n in 128 299; do TCI_LIB=build/ab/libtci_chainprof.so timeout -k 10 60 python scripts/dram_time.py 20000 fused 20 $n || exit 1; done
+bash scripts/gpu_dram_check.sh dr10 || exit 1
+TCI_LIB=build/ab/libtci_adaptprof.so timeout -k 10 60 python scripts/dram_time.py 20000 fused 20
+VARIANTS="ship" bash scripts/gpu_dram_ab.sh dab10 20000

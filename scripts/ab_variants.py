@@ -26,6 +26,8 @@ VARIANTS = {
     "loopramp": ["TCI_RAMP_PREFIX=0"],
     "abl_loads": ["TCI_ABLATE=16"],
     "chainprof": ["TCI_CHAIN_PROFILE=1"],
+    "adaptprof": ["TCI_ADAPT_PROFILE=1"],
+    "adapt_twice": ["TCI_ADAPT_TWICE=1"],
     "adapt_nochol": ["TCI_ADAPT_ABLATE=1"],
     "adapt_nocov": ["TCI_ADAPT_ABLATE=2"],
     "draws_nonorm": ["TCI_DRAWS_ABLATE=1"],

@@ -584,6 +584,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(cmean, double, n * L);
   TCI_ALLOC(wsum, double, n);
   TCI_ALLOC(window, double, n * (size_t)win * L);
+  TCI_ALLOC(wsumv, double, n * L);
   TCI_ALLOC(prop1, double, n * L);
   TCI_ALLOC(prop2, double, n * L);
   TCI_ALLOC(act1, uint8_t, n);
@@ -602,7 +603,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(sq_mean, double, n);
   TCI_ALLOC(sq_m2, double, n);
   TCI_ALLOC(step, int64_t, 1);
-#ifdef TCI_CHAIN_PROFILE
+#if defined(TCI_CHAIN_PROFILE) || defined(TCI_ADAPT_PROFILE)
   TCI_ALLOC(prof, int64_t, 8);
   TCI_HIP(ctx, hipMemsetAsync(st.prof, 0, 8 * sizeof(int64_t), ctx->stream));
 #endif
@@ -723,7 +724,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_HIP(ctx, hipStreamSynchronize(s));
   if (exec) (void)hipGraphExecDestroy(exec);
   if (graph) (void)hipGraphDestroy(graph);
-#ifdef TCI_CHAIN_PROFILE
+#if defined(TCI_CHAIN_PROFILE) || defined(TCI_ADAPT_PROFILE)
   {
     int64_t ph[8];
     TCI_HIP(ctx, hipMemcpy(ph, st.prof, sizeof(ph), hipMemcpyDeviceToHost));

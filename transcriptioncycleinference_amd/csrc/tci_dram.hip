@@ -378,8 +378,13 @@ __device__ void record_vec(const DramState& st, const DramParams& p, int64_t c, 
                            double* smean, double* sm2, int j0, int js) {
   const int64_t ld = st.ld;
   if (p.adaptint > 0) {
-    double* w = st.window + (c * p.adaptint + (row - 1) % p.adaptint) * ld;
-    for (int j = j0; j < P; j += js) w[j] = th[j];
+    const int64_t slot = (row - 1) % p.adaptint;
+    double* w = st.window + (c * p.adaptint + slot) * ld;
+    double* ws = st.wsumv + c * ld;  // the window's column sums, in row order (adaptation's batch mean)
+    for (int j = j0; j < P; j += js) {
+      w[j] = th[j];
+      ws[j] = slot == 0 ? th[j] : ws[j] + th[j];
+    }
   }
   if (row >= p.stats_from) {  // posterior mean / population std over chain(stats_from:end, :) (:276-301)
     const double n = (double)(row - p.stats_from + 1);
@@ -780,14 +785,16 @@ struct RowCursor {
 // stores and Welford arithmetic as record_vec.
 template <int NJ>
 __device__ __forceinline__ void record_vec_reg(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P,
-                                               const double* th, double* smn, double* sm2, int lane,
-                                               const RowCursor& cur) {
+                                               const double* th, double* smn, double* sm2, double* wsv,
+                                               int lane, const RowCursor& cur) {
   const int64_t ld = st.ld;
   if (p.adaptint > 0) {
     double* w = st.window + (c * p.adaptint + cur.win) * ld;
 #pragma unroll
-    for (int k = 0; k < NJ; ++k)
+    for (int k = 0; k < NJ; ++k) {
       if (lane + 64 * k < P) w[lane + 64 * k] = th[k];
+      wsv[k] = cur.win == 0 ? th[k] : wsv[k] + th[k];  // as record_vec's column sums
+    }
   }
   if (row >= p.stats_from) {
     const double n = (double)(row - p.stats_from + 1);
@@ -823,8 +830,11 @@ __device__ __forceinline__ void record_s2_cur(const DramState& st, const DramPar
 #ifndef TCI_CHAIN_PROFILE
 #define TCI_CHAIN_PROFILE 0  // diagnostics: s_memtime cycles per k_chain phase (wave 0) into st.prof
 #endif
+#ifndef TCI_ADAPT_PROFILE
+#define TCI_ADAPT_PROFILE 0  // diagnostics: s_memtime cycles per k_adapt_mfma phase (thread 0) into st.prof
+#endif
 __device__ __forceinline__ uint64_t stamp() {
-#if TCI_CHAIN_PROFILE
+#if TCI_CHAIN_PROFILE || TCI_ADAPT_PROFILE
   uint64_t t;
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -862,7 +872,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
   const int stage = w & 1, ahead = w >> 1;                        // this wave's proposal
   const double scale = stage ? 1.0 / p.drscale : 1.0;
-  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], smn[NJ], sm2[NJ];
+  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], smn[NJ], sm2[NJ], wsv[NJ];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
     const int j = lane + 64 * k;
@@ -872,10 +882,11 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     hi[k] = in ? st.upper[c * ld + j] : 0.0;
     mu[k] = in ? st.pmu[c * ld + j] : 0.0;
     sg[k] = in ? st.psig[c * ld + j] : 0.0;
-    smn[k] = sm2[k] = 0.0;
-    if (w == 0 && in) {  // wave 0 keeps the posterior Welford statistics
+    smn[k] = sm2[k] = wsv[k] = 0.0;
+    if (w == 0 && in) {  // wave 0 keeps the posterior Welford statistics and the window sums
       smn[k] = st.smean[c * ld + j];
       sm2[k] = st.sm2[c * ld + j];
+      wsv[k] = st.wsumv[c * ld + j];
     }
   }
   EvalIn<RPL> e;  // the chain's cell records stay in registers
@@ -1026,7 +1037,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       if (p.updatesigma) s2 = hh ? (acc ? s2_4 : acc2 ? s2_5 : s2_3) : (acc ? s2_1 : acc2 ? s2_2 : s2_0);
       // the row's records
       const int64_t row = s + hh;
-      if (w == 0) record_vec_reg<NJ>(st, p, c, row, P, th, smn, sm2, lane, cur);
+      if (w == 0) record_vec_reg<NJ>(st, p, c, row, P, th, smn, sm2, wsv, lane, cur);
       if (w == 1 && lane == 0) record_s2_cur(st, p, c, row, s2, s2a, cur);
       cur.next(p);
       adv = hh + 1;
@@ -1062,6 +1073,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
         st.theta[c * ld + j] = th[k];
         st.smean[c * ld + j] = smn[k];
         st.sm2[c * ld + j] = sm2[k];
+        st.wsumv[c * ld + j] = wsv[k];
       }
     }
     if (lane == 0) {
@@ -1343,6 +1355,259 @@ __global__ __launch_bounds__(kThreads) void k_adapt_tiles(DramState st, DramPara
   if (t == 0) st.nrej_win[c] = 0;
 }
 
+// ---- Adaptation on matrix cores, for P <= 16 * kAdM (every TestData cell). One workgroup per
+// chain; the upper triangle of cov + qcovadj I lives in LDS as 16 x 16 tiles.
+//   covupd: the window's rows, centred on their batch mean and staged through LDS, give the scatter
+//     S = Xc' Xc as v_mfma_f64_16x16x4_f64 products (each wave owns every 4th output tile), merged
+//     into (cov, mean, wsum) by the pairwise-update formula (the same numbers as mcmcstat's
+//     row-by-row recurrence in exact arithmetic);
+//   Cholesky cov + qcovadj I = U'U, right-looking by 16-column panels: wave 0 factors the diagonal
+//     tile, 16-lane groups solve the panel's row tiles (one column per lane), and the trailing
+//     tiles take the rank-16 update as 4 MFMAs each. R = U * adascale.
+constexpr int kAdM = 9;     // max tiles per dimension (P <= 144)
+constexpr int kAdRB = 32;   // window rows per LDS batch
+constexpr int kAdOwn = 12;  // output tiles per wave: kAdM (kAdM + 1) / 2 <= 4 kAdOwn
+__host__ __device__ inline int ad_tile(int ti, int tj, int NT) { return ti * NT - ti * (ti - 1) / 2 + (tj - ti); }
+__host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P) {
+  const int64_t NT = (P + 15) / 16, T = NT * (NT + 1) / 2, LX = 16 * NT;
+  return (T * 256 + kAdRB * LX + 2 * LX) * 8;
+}
+
+__global__ __launch_bounds__(kThreads) void k_adapt_mfma(DramState st, DramParams p) {
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  __shared__ int fail;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int row = lane & 15, kq = lane >> 4;
+  const int64_t c = blockIdx.x;
+  const int64_t step = *st.step;
+  if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
+  const int64_t ld = st.ld;
+  const int P = st.npar[c];
+  const int NT = (P + 15) >> 4, LX = 16 * NT, T = NT * (NT + 1) / 2;
+  double* Tl = dyn;               // T tiles of 256 (row-major inside a tile)
+  double* X = Tl + T * 256;       // a batch of centred window rows [kAdRB][LX]
+  double* mb = X + kAdRB * LX;    // batch mean
+  double* mo = mb + LX;           // old mean
+  double* cvg = st.cov + c * ld * ld;
+  double* mu = st.cmean + c * ld;
+  const int nb = (int)p.adaptint;
+  const double* win = st.window + c * p.adaptint * ld;
+  uint64_t aph[6] = {0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
+#define TCI_APHASE(k) \
+  if (TCI_ADAPT_PROFILE) { a1 = stamp(); aph[k] += a1 - a0; a0 = a1; }
+  // ---- batch mean from the window's column sums (kept by the engines as rows are recorded)
+  for (int j = t; j < LX; j += kThreads) {
+    mb[j] = j < P ? st.wsumv[c * ld + j] / (double)nb : 0.0;
+    mo[j] = j < P ? mu[j] : 0.0;
+  }
+  // owned output tiles (ti <= tj): every 4th of the row-major tile order, from w. Slots past the
+  // last tile compute on tile (0, 0) and are discarded, so the code is straight-line and every
+  // array index is a compile-time constant (no scratch memory).
+  int sti[kAdOwn], stj[kAdOwn];
+#pragma unroll
+  for (int o = 0; o < kAdOwn; ++o) {
+    int k = w + 4 * o, ti = 0;
+    if (k >= T) k = 0;
+    while (k >= NT - ti) {  // uniform
+      k -= NT - ti;
+      ++ti;
+    }
+    sti[o] = ti;
+    stj[o] = ti + k;
+  }
+  const int nown = (T - w + 3) / 4;  // valid slots
+  // ---- pass 2: scatter of the centred rows on MFMA
+  f64x4 acc[kAdOwn];
+#pragma unroll
+  for (int o = 0; o < kAdOwn; ++o) acc[o] = f64x4{0.0, 0.0, 0.0, 0.0};
+  __syncthreads();
+  for (int r0 = 0; r0 < nb; r0 += kAdRB) {
+    const int n = min(kAdRB, nb - r0);
+    // all of this thread's loads first, then the LDS stores (kAdRB * LX / 256 <= 18 per thread)
+    constexpr int kPer = (kAdRB * 16 * kAdM + kThreads - 1) / kThreads;
+    double v[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int e = t + u * kThreads, r = e / LX, j = e - r * LX;
+      v[u] = (e < kAdRB * LX && r < n && j < P) ? win[(int64_t)(r0 + r) * ld + j] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int e = t + u * kThreads, r = e / LX, j = e - r * LX;
+      if (e < kAdRB * LX) X[e] = (r < n && j < P) ? v[u] - mb[j] : 0.0;
+    }
+    __syncthreads();
+    for (int k0 = 0; k0 < n; k0 += 4) {
+      const double* xr = X + (k0 + kq) * LX + row;
+      double xa[kAdOwn], xb[kAdOwn];
+#pragma unroll
+      for (int o = 0; o < kAdOwn; ++o) {
+        xa[o] = xr[16 * sti[o]];
+        xb[o] = xr[16 * stj[o]];
+      }
+#pragma unroll
+      for (int o = 0; o < kAdOwn; ++o) acc[o] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[o], xb[o], acc[o], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  TCI_APHASE(1)
+  // ---- merge (cov, mean, wsum) with the batch: n = na + nb, d = m_batch - m_old; tiles of the
+  //      matrix to factor: cov + qcovadj I (identity in the padding)
+  const double na = st.wsum[c], nn = na + (double)nb;
+  const double fcross = na * (double)nb / nn;
+  double old[kAdOwn][4];  // every old value is read before any is written (diagonal tiles read mirrors)
+#pragma unroll
+  for (int o = 0; o < kAdOwn; ++o)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = 16 * sti[o] + kq + 4 * q, j = 16 * stj[o] + row;
+      old[o][q] = (i < P && j < P && na > 0.0) ? cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i] : 0.0;
+    }
+#pragma unroll
+  for (int o = 0; o < kAdOwn; ++o) {
+    if (o >= nown) continue;  // uniform
+    double* tile = Tl + ad_tile(sti[o], stj[o], NT) * 256;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int il = kq + 4 * q, jl = row;
+      const int i = 16 * sti[o] + il, j = 16 * stj[o] + jl;
+      double a;
+      if (i < P && j < P) {
+        double cv;
+        if (nn <= 1.0) {
+          cv = 0.0;  // a single row so far: covariance 0 (the recurrence's first row)
+        } else if (na == 0.0) {
+          cv = acc[o][q] / (nn - 1.0);
+        } else {
+          const double di = mb[i] - mo[i], dj = mb[j] - mo[j];
+          cv = (old[o][q] * (na - 1.0) + acc[o][q] + di * dj * fcross) / (nn - 1.0);
+        }
+        if (i <= j) cvg[(int64_t)i * ld + j] = cv;
+        a = cv + (i == j ? p.qcovadj : 0.0);
+      } else {
+        a = i == j ? 1.0 : 0.0;
+      }
+      tile[il * 16 + jl] = a;
+    }
+  }
+  __syncthreads();  // cvg reads (lower half of diagonal tiles) before anything else; tiles complete
+  for (int j = t; j < P; j += kThreads) mu[j] = na == 0.0 ? mb[j] : mo[j] + (mb[j] - mo[j]) * ((double)nb / nn);
+  if (t == 0) {
+    st.wsum[c] = nn;
+    fail = 0;
+  }
+  if (step < p.burnintime) {
+    // burn-in: no covariance adaptation, only scaling by the window's rejection rate
+    const double rate = (double)st.nrej_win[c] / (double)p.adaptint;
+    double s = 1.0;
+    if (rate > 0.95) s = 1.0 / p.burnin_scale;
+    else if (rate < 0.05) s = p.burnin_scale;
+    if (s != 1.0) {
+      double* R = st.R + c * ld * ld;
+      for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
+        const int i = (int)(e / P), j = (int)(e % P);
+        store_R(st, c, P, i, j, f32_round(R[(int64_t)i * ld + j] * s));
+      }
+    }
+    __syncthreads();
+    if (t == 0) st.nrej_win[c] = 0;
+    return;
+  }
+  __syncthreads();
+  TCI_APHASE(2)
+  // ---- blocked Cholesky U'U of the tiles, in place (upper tiles become U)
+  for (int pk = 0; pk < NT; ++pk) {
+    double* D = Tl + ad_tile(pk, pk, NT) * 256;
+    // (1) the diagonal tile, by wave 0: 16 right-looking steps on LDS
+    if (w == 0) {
+      for (int k = 0; k < 16; ++k) {
+        const double d = D[k * 17];
+        if (!(d > 0.0) || !isfinite(d)) {
+          if (lane == 0) fail = 1;
+          break;  // uniform
+        }
+        const double rs = 1.0 / sqrt(d);
+        double ui[4], uj[4], dij[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int e = lane + 64 * m, i = e >> 4, j = e & 15;
+          ui[m] = D[k * 16 + i];
+          uj[m] = D[k * 16 + j];
+          dij[m] = D[e];
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int e = lane + 64 * m, i = e >> 4, j = e & 15;
+          if (i > k && j >= i) D[e] = dij[m] - (ui[m] * rs) * (uj[m] * rs);
+          else if (i == k && j >= k) D[e] = uj[m] * rs;
+        }
+        wave_sync();
+      }
+    }
+    __syncthreads();
+    if (fail) break;
+    // (2) the panel's row tiles (pk, tj > pk): U_pk' X = A -> X, one column per lane, 4 tiles per wave
+    {
+      const int g = w * 4 + kq;  // 16-lane group 0..15
+      for (int tj = pk + 1 + g; tj < NT; tj += 16) {
+        double* A = Tl + ad_tile(pk, tj, NT) * 256;
+        double x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = A[k * 16 + row];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          x[k] = x[k] / D[k * 17];
+#pragma unroll
+          for (int m = k + 1; m < 16; ++m) x[m] = fma(-D[k * 16 + m], x[k], x[m]);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) A[k * 16 + row] = x[k];
+      }
+    }
+    __syncthreads();
+    // (3) trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj (rank-16, 4 MFMAs), every 4th per wave
+    {
+      const int m = NT - 1 - pk, TT = m * (m + 1) / 2;
+      int ti = pk + 1, tj = pk + 1;
+      for (int k = 0; k < TT; ++k) {
+        if ((k & 3) == w) {
+          double* C = Tl + ad_tile(ti, tj, NT) * 256;
+          const double* Xi = Tl + ad_tile(pk, ti, NT) * 256;
+          const double* Xj = Tl + ad_tile(pk, tj, NT) * 256;
+          f64x4 cacc;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) cacc[q] = C[(kq + 4 * q) * 16 + row];
+#pragma unroll
+          for (int k4 = 0; k4 < 16; k4 += 4)
+            cacc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Xi[(k4 + kq) * 16 + row], Xj[(k4 + kq) * 16 + row], cacc, 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) C[(kq + 4 * q) * 16 + row] = cacc[q];
+        }
+        if (++tj == NT) tj = ++ti;
+      }
+    }
+    __syncthreads();
+  }
+  TCI_APHASE(3)
+  if (!fail) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
+    const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
+    const int il = t >> 4, jl = t & 15;  // one element of every upper tile per thread
+#pragma unroll 4
+    for (int ti = 0; ti < NT; ++ti)
+      for (int tj = ti; tj < NT; ++tj) {
+        const int i = 16 * ti + il, j = 16 * tj + jl;
+        if (i < P && j < P && j >= i) store_R(st, c, P, i, j, f32_round(Tl[ad_tile(ti, tj, NT) * 256 + t] * sc));
+      }
+  }
+  __syncthreads();
+  TCI_APHASE(4)
+#undef TCI_APHASE
+  if (TCI_ADAPT_PROFILE && t == 0 && st.prof != nullptr)
+    for (int q = 0; q < 5; ++q) atomicAdd((unsigned long long*)&st.prof[q], (unsigned long long)aph[q]);
+  if (t == 0) st.nrej_win[c] = 0;
+}
+
 inline int finish() { return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP; }
 inline dim3 chain_grid(int64_t n) { return dim3((unsigned)n); }
 
@@ -1375,6 +1640,17 @@ int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream) 
   return launch_stage(k_accept2, st, p, stream);
 }
 int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
+  if (p.pmax <= 16 * kAdM) {
+    const size_t bytes = (size_t)adapt_mfma_lds_bytes(p.pmax);
+    if (bytes > 48 * 1024 && hipFuncSetAttribute((const void*)k_adapt_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)bytes) != hipSuccess)
+      return TCI_EHIP;
+    hipLaunchKernelGGL(k_adapt_mfma, chain_grid(st.n_chains), dim3(kThreads), bytes, (hipStream_t)stream, st, p);
+#ifdef TCI_ADAPT_TWICE  // diagnostics only (wrong results): a second, warm launch of the same kernel
+    hipLaunchKernelGGL(k_adapt_mfma, chain_grid(st.n_chains), dim3(kThreads), bytes, (hipStream_t)stream, st, p);
+#endif
+    return finish();
+  }
   const int64_t ntile = (p.pmax + 3) / 4;
   if (ntile * (ntile + 1) / 2 <= (int64_t)kAdaptTiles * kThreads && adapt_tiles_lds_bytes(p.pmax) <= 78 * 1024) {
     const size_t bytes = (size_t)adapt_tiles_lds_bytes(p.pmax);

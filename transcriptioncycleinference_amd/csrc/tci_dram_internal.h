@@ -31,6 +31,7 @@ struct DramState {
   double* cmean;
   double* wsum;
   double* window;          // the last adaptint chain rows (for covupd)
+  double* wsumv;           // column sums of the window's rows so far (row order; the adaptation's batch mean)
   double* prop1;           // stage-1 / stage-2 proposals (n_chains x ld)
   double* prop2;
   uint8_t* act1;           // in-bounds flags (ssfun is called only for these)
