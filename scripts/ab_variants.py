@@ -34,6 +34,9 @@ VARIANTS = {
     "draws_nomfma": ["TCI_DRAWS_ABLATE=2"],
     "draws_noscal": ["TCI_DRAWS_ABLATE=4"],
     "draws_noR": ["TCI_DRAWS_ABLATE=8"],
+    "draws_p4": ["TCI_DRAW_PASSES=4"],
+    "draws_p7": ["TCI_DRAW_PASSES=7"],
+    "draws_p1": ["TCI_DRAW_PASSES=1"],
 }
 
 

@@ -214,7 +214,8 @@ __device__ void load_R_f32(float* Rl, const DramState& st, int64_t c, int P) {
 // One v_mfma_f64_16x16x4_f64 per 4-row k-step of a 16 x 16 (row tile, column tile) block:
 // A = Z[row = lane&15][k = lane>>4], B = R[k = lane>>4][col = lane&15], D row = (lane>>4) + 4 q,
 // col = lane&15 (cdna_hip_programming.md f64 MFMA map). Column tiles go to the 4 waves in snake order
-// (balanced triangle costs); a wave runs its (up to CT) column tiles x MT row tiles together, so one
+// from the last (costliest) tile down (balanced triangle costs: 12/11/11/11 k-step units for 9 tiles,
+// where ascending order gave one wave 18); a wave runs its (up to CT) column tiles x MT row tiles together, so one
 // A and one B fragment load feed CT*MT independent MFMA chains. Each tile skips the k-steps below
 // the triangle. A product depends only on its row of Z and the fixed k order, so every MT/CT
 // instance (the batched engine's 1-row proposals, the fused engine's 32-row draws) gives the same
@@ -229,8 +230,8 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
   int kend = -1;
 #pragma unroll
   for (int g = 0; g < CT; ++g) {
-    nt[g] = 4 * g + ((g & 1) ? 3 - w : w);  // uniform
-    kmx[g] = nt[g] < ntiles ? min(16 * nt[g] + 15, P - 1) : -1;
+    nt[g] = ntiles - 1 - (4 * g + ((g & 1) ? 3 - w : w));  // uniform: costliest tiles first, snake order
+    kmx[g] = nt[g] >= 0 ? min(16 * nt[g] + 15, P - 1) : -1;
     kend = max(kend, kmx[g]);
   }
   f64x4 acc[CT][MT];
@@ -251,7 +252,7 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
     const int toff = tri_off(ic, P) - ic;
 #pragma unroll
     for (int g = 0; g < CT; ++g) {
-      if (i0 > kmx[g]) continue;  // uniform
+      if (i0 > kmx[g]) continue;  // uniform (invalid tiles: kmx = -1)
       const int j = 16 * nt[g] + row;
       const int jc = j < P ? j : P - 1;
       const float rv = Rl[toff + (jc >= ic ? jc : ic)];
@@ -695,7 +696,10 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
 #endif
 constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each)
 constexpr int kDrawSteps = 8 * kDrawMT;   // steps per pass (2 rows per step)
-constexpr int kDrawPasses = 2;            // passes per k_draws workgroup (32 steps)
+#ifndef TCI_DRAW_PASSES
+#define TCI_DRAW_PASSES 2
+#endif
+constexpr int kDrawPasses = TCI_DRAW_PASSES;  // passes per k_draws workgroup (32 steps)
 enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
 
 // Dynamic LDS of k_draws: one pass's normals (2 x kDrawSteps rows of stride L) and the chain's R
@@ -1355,27 +1359,87 @@ __global__ __launch_bounds__(kThreads) void k_adapt_tiles(DramState st, DramPara
   if (t == 0) st.nrej_win[c] = 0;
 }
 
-// ---- Adaptation on matrix cores, for P <= 16 * kAdM (every TestData cell). One workgroup per
-// chain; the upper triangle of cov + qcovadj I lives in LDS as 16 x 16 tiles.
-//   covupd: the window's rows, centred on their batch mean and staged through LDS, give the scatter
-//     S = Xc' Xc as v_mfma_f64_16x16x4_f64 products (each wave owns every 4th output tile), merged
-//     into (cov, mean, wsum) by the pairwise-update formula (the same numbers as mcmcstat's
-//     row-by-row recurrence in exact arithmetic);
-//   Cholesky cov + qcovadj I = U'U, right-looking by 16-column panels: wave 0 factors the diagonal
-//     tile, 16-lane groups solve the panel's row tiles (one column per lane), and the trailing
-//     tiles take the rank-16 update as 4 MFMAs each. R = U * adascale.
-constexpr int kAdM = 9;     // max tiles per dimension (P <= 144)
-constexpr int kAdRB = 32;   // window rows per LDS batch
-constexpr int kAdOwn = 12;  // output tiles per wave: kAdM (kAdM + 1) / 2 <= 4 kAdOwn
-__host__ __device__ inline int ad_tile(int ti, int tj, int NT) { return ti * NT - ti * (ti - 1) / 2 + (tj - ti); }
-__host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P) {
-  const int64_t NT = (P + 15) / 16, T = NT * (NT + 1) / 2, LX = 16 * NT;
-  return (T * 256 + kAdRB * LX + 2 * LX) * 8;
+// Lane (16 g + K)'s x in every lane of 16-lane row g (DPP row_newbcast, no LDS).
+template <int K>
+__device__ __forceinline__ double row_bcast16(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x150 + K, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x150 + K, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
 }
 
-__global__ __launch_bounds__(kThreads) void k_adapt_mfma(DramState st, DramParams p) {
+// Step K of the Cholesky factorization A = U'U of a symmetric 16 x 16 tile held by ONE wave in
+// registers, in the MFMA accumulator layout (lane 16 g + j holds rows g, g+4, g+8, g+12 of
+// column j). Rows and columns > K take the symmetric rank-1 update A -= a_K a_K' / d (both
+// triangles, so column K is a row broadcast: A[i][K] = A[K][i]); row K keeps A[K][j] and its pivot
+// d goes to dpiv[K]. The dependent chain per step is a readlane, a reciprocal (v_rcp_f64 and one
+// Newton step) and one FMA; the square roots are left to chol16_finish.
+template <int K>
+__device__ __forceinline__ void chol16_step(double (&a)[4], int lane, double* dpiv, bool& bad) {
+  if constexpr (K < 16) {
+    constexpr int kg = K & 3, kr = K >> 2;
+    const int g = lane >> 4, j = lane & 15;
+    const double d = lane_bcast(a[kr], 16 * kg + K);
+    bad = bad || !(d > 0.0) || !isfinite(d);
+    double rd = __builtin_amdgcn_rcp(d);
+    rd = fma(rd, fma(-d, rd, 1.0), rd);
+    const double akj = __shfl(a[kr], 16 * kg + j);  // A[K][j]
+    double aik[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) aik[q] = row_bcast16<K>(a[q]);  // A[g + 4q][K]
+    const double sj = akj * rd;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (g + 4 * q > K && j > K) a[q] = fma(-aik[q], sj, a[q]);
+    if (lane == 0) dpiv[K] = d;
+    chol16_step<K + 1>(a, lane, dpiv, bad);
+  }
+}
+
+// After the 16 steps: U[i][j] = A[i][j] / sqrt(d_i) for j >= i; rdg[i] = 1 / U[i][i] for the panel
+// solve (dpiv and rdg may alias: each lane reads its pivots before the diagonal lanes write).
+__device__ __forceinline__ void chol16_finish(double (&a)[4], int lane, double* dpiv, double* rdg) {
+  const int g = lane >> 4, j = lane & 15;
+  double rs[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) rs[q] = 1.0 / sqrt(dpiv[g + 4 * q]);
+  wave_sync();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    a[q] = a[q] * rs[q];
+    if (j == g + 4 * q) rdg[j] = rs[q];
+  }
+}
+
+// ---- Adaptation on matrix cores, for P <= 16 * kAdM (every TestData cell). One workgroup per
+// chain. The upper triangle of cov + qcovadj I is held as 16 x 16 tiles in the MFMA accumulator
+// layout, in REGISTERS: wave w owns every 4th tile of the row-major tile order for the whole
+// kernel. LDS holds only one batch of window rows (scatter) or, aliased onto it, two panel
+// buffers (Cholesky): ~39 KB, so two chains' workgroups share a CU and all 299 TestData chains are
+// resident at once (a 131 KB tile-in-LDS layout ran them in two rounds on 256 CUs).
+//   covupd: the window's rows, centred on their batch mean and staged through LDS (the next batch
+//     is loaded while the current one is multiplied), give the scatter S = Xc' Xc as
+//     v_mfma_f64_16x16x4_f64 products into the owned tiles, merged with (cov, mean, wsum) by the
+//     pairwise-update formula (mcmcstat's row-by-row recurrence in exact arithmetic);
+//   Cholesky cov + qcovadj I = U'U, right-looking by 16-column panels: the owners copy panel row pk
+//     to LDS (the diagonal tile factored on the way, in its owner's registers: chol16_step),
+//     16-lane groups solve the panel's row tiles (one column per lane), the owners take their U
+//     tiles back and every trailing tile takes the rank-16 update as 4 MFMAs on its owner's
+//     registers. R = U * adascale, stored only when the
+//     whole factorization succeeded (a singular matrix keeps the previous R, as mcmcstat).
+constexpr int kAdM = 9;     // max tiles per dimension (P <= 144)
+constexpr int kAdRB = 16;   // window rows per LDS batch
+constexpr int kAdOwn = 12;  // output tiles per wave: kAdM (kAdM + 1) / 2 <= 4 kAdOwn
+__host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P) {
+  const int64_t NT = (P + 15) / 16, LX = 16 * NT;
+  const int64_t shared = kAdRB * LX > 2 * NT * 256 ? kAdRB * LX : 2 * NT * 256;  // X | panel buffers
+  return (shared + 2 * LX) * 8;
+}
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_adapt_mfma(DramState st,
+                                                                                                 DramParams p) {
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int fail;
+  __shared__ double rdg[16];  // 1 / U[k][k] of the current diagonal tile
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int row = lane & 15, kq = lane >> 4;
@@ -1385,25 +1449,26 @@ __global__ __launch_bounds__(kThreads) void k_adapt_mfma(DramState st, DramParam
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int NT = (P + 15) >> 4, LX = 16 * NT, T = NT * (NT + 1) / 2;
-  double* Tl = dyn;               // T tiles of 256 (row-major inside a tile)
-  double* X = Tl + T * 256;       // a batch of centred window rows [kAdRB][LX]
-  double* mb = X + kAdRB * LX;    // batch mean
+  const int shared = max(kAdRB * LX, 2 * NT * 256);
+  double* X = dyn;                // scatter: a batch of centred window rows [kAdRB][LX]
+  double* Pb = dyn;               // Cholesky: panel buffers [2][NT][256] (aliases X)
+  double* mb = dyn + shared;      // batch mean
   double* mo = mb + LX;           // old mean
   double* cvg = st.cov + c * ld * ld;
   double* mu = st.cmean + c * ld;
-  const int nb = (int)p.adaptint;
+  const int nb = (TCI_ADAPT_ABLATE & 2) ? 0 : (int)p.adaptint;
   const double* win = st.window + c * p.adaptint * ld;
   uint64_t aph[6] = {0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
 #define TCI_APHASE(k) \
   if (TCI_ADAPT_PROFILE) { a1 = stamp(); aph[k] += a1 - a0; a0 = a1; }
   // ---- batch mean from the window's column sums (kept by the engines as rows are recorded)
   for (int j = t; j < LX; j += kThreads) {
-    mb[j] = j < P ? st.wsumv[c * ld + j] / (double)nb : 0.0;
+    mb[j] = j < P ? st.wsumv[c * ld + j] / (double)p.adaptint : 0.0;
     mo[j] = j < P ? mu[j] : 0.0;
   }
-  // owned output tiles (ti <= tj): every 4th of the row-major tile order, from w. Slots past the
-  // last tile compute on tile (0, 0) and are discarded, so the code is straight-line and every
-  // array index is a compile-time constant (no scratch memory).
+  // owned tiles (ti <= tj): every 4th of the row-major tile order, from w. Slots past the last
+  // tile compute on tile (0, 0) and are discarded, so the code is straight-line and every array
+  // index is a compile-time constant (the tiles stay in registers, no scratch memory).
   int sti[kAdOwn], stj[kAdOwn];
 #pragma unroll
   for (int o = 0; o < kAdOwn; ++o) {
@@ -1417,27 +1482,31 @@ __global__ __launch_bounds__(kThreads) void k_adapt_mfma(DramState st, DramParam
     stj[o] = ti + k;
   }
   const int nown = (T - w + 3) / 4;  // valid slots
-  // ---- pass 2: scatter of the centred rows on MFMA
+  // ---- scatter of the centred rows on MFMA; batch r0 + kAdRB is loaded while r0 is multiplied
   f64x4 acc[kAdOwn];
 #pragma unroll
   for (int o = 0; o < kAdOwn; ++o) acc[o] = f64x4{0.0, 0.0, 0.0, 0.0};
-  __syncthreads();
-  for (int r0 = 0; r0 < nb; r0 += kAdRB) {
+  constexpr int kPer = (kAdRB * 16 * kAdM + kThreads - 1) / kThreads;
+  double v[kPer];
+  auto load_batch = [&](int r0) {
     const int n = min(kAdRB, nb - r0);
-    // all of this thread's loads first, then the LDS stores (kAdRB * LX / 256 <= 18 per thread)
-    constexpr int kPer = (kAdRB * 16 * kAdM + kThreads - 1) / kThreads;
-    double v[kPer];
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int e = t + u * kThreads, r = e / LX, j = e - r * LX;
       v[u] = (e < kAdRB * LX && r < n && j < P) ? win[(int64_t)(r0 + r) * ld + j] : 0.0;
     }
+  };
+  if (nb > 0) load_batch(0);
+  __syncthreads();  // mb
+  for (int r0 = 0; r0 < nb; r0 += kAdRB) {
+    const int n = min(kAdRB, nb - r0);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int e = t + u * kThreads, r = e / LX, j = e - r * LX;
       if (e < kAdRB * LX) X[e] = (r < n && j < P) ? v[u] - mb[j] : 0.0;
     }
     __syncthreads();
+    if (r0 + kAdRB < nb) load_batch(r0 + kAdRB);
     for (int k0 = 0; k0 < n; k0 += 4) {
       const double* xr = X + (k0 + kq) * LX + row;
       double xa[kAdOwn], xb[kAdOwn];
@@ -1452,47 +1521,56 @@ __global__ __launch_bounds__(kThreads) void k_adapt_mfma(DramState st, DramParam
     __syncthreads();
   }
   TCI_APHASE(1)
-  // ---- merge (cov, mean, wsum) with the batch: n = na + nb, d = m_batch - m_old; tiles of the
-  //      matrix to factor: cov + qcovadj I (identity in the padding)
-  const double na = st.wsum[c], nn = na + (double)nb;
-  const double fcross = na * (double)nb / nn;
-  double old[kAdOwn][4];  // every old value is read before any is written (diagonal tiles read mirrors)
+  // ---- merge (cov, mean, wsum) with the batch: n = na + nb, d = m_batch - m_old; the owned tiles
+  //      become the matrix to factor: cov + qcovadj I (identity in the padding)
+  const double na = st.wsum[c], nn = na + (double)p.adaptint;
+  const double fcross = na * (double)p.adaptint / nn;
+  // in groups of kAdMG tiles: a group's old values are all read before any of them is written (a
+  // diagonal tile reads the mirrors of its own elements)
+  const double rn1 = 1.0 / (nn - 1.0);
+  constexpr int kAdMG = 6;
 #pragma unroll
-  for (int o = 0; o < kAdOwn; ++o)
+  for (int o0 = 0; o0 < kAdOwn; o0 += kAdMG) {
+    if (o0 >= nown) break;  // uniform
+    double old[kAdMG][4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = 16 * sti[o] + kq + 4 * q, j = 16 * stj[o] + row;
-      old[o][q] = (i < P && j < P && na > 0.0) ? cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i] : 0.0;
-    }
+    for (int u = 0; u < kAdMG; ++u)
 #pragma unroll
-  for (int o = 0; o < kAdOwn; ++o) {
-    if (o >= nown) continue;  // uniform
-    double* tile = Tl + ad_tile(sti[o], stj[o], NT) * 256;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int il = kq + 4 * q, jl = row;
-      const int i = 16 * sti[o] + il, j = 16 * stj[o] + jl;
-      double a;
-      if (i < P && j < P) {
-        double cv;
-        if (nn <= 1.0) {
-          cv = 0.0;  // a single row so far: covariance 0 (the recurrence's first row)
-        } else if (na == 0.0) {
-          cv = acc[o][q] / (nn - 1.0);
-        } else {
-          const double di = mb[i] - mo[i], dj = mb[j] - mo[j];
-          cv = (old[o][q] * (na - 1.0) + acc[o][q] + di * dj * fcross) / (nn - 1.0);
-        }
-        if (i <= j) cvg[(int64_t)i * ld + j] = cv;
-        a = cv + (i == j ? p.qcovadj : 0.0);
-      } else {
-        a = i == j ? 1.0 : 0.0;
+      for (int q = 0; q < 4; ++q) {
+        const int o = o0 + u, i = 16 * sti[o] + kq + 4 * q, j = 16 * stj[o] + row;
+        old[u][q] = (o < nown && i < P && j < P && na > 0.0) ? cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i]
+                                                            : 0.0;
       }
-      tile[il * 16 + jl] = a;
+#pragma unroll
+    for (int u = 0; u < kAdMG; ++u) {
+      const int o = o0 + u;
+      if (o >= nown) continue;  // uniform
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 16 * sti[o] + kq + 4 * q, j = 16 * stj[o] + row;
+        double a;
+        if (i < P && j < P) {
+          double cv;
+          if (nn <= 1.0) {
+            cv = 0.0;  // a single row so far: covariance 0 (the recurrence's first row)
+          } else if (na == 0.0) {
+            cv = acc[o][q] * rn1;
+          } else {
+            const double di = mb[i] - mo[i], dj = mb[j] - mo[j];
+            cv = (old[u][q] * (na - 1.0) + acc[o][q] + di * dj * fcross) * rn1;
+          }
+          if (i <= j) cvg[(int64_t)i * ld + j] = cv;
+          a = cv + (i == j ? p.qcovadj : 0.0);
+        } else {
+          a = i == j ? 1.0 : 0.0;
+        }
+        acc[o][q] = a;
+      }
     }
   }
-  __syncthreads();  // cvg reads (lower half of diagonal tiles) before anything else; tiles complete
-  for (int j = t; j < P; j += kThreads) mu[j] = na == 0.0 ? mb[j] : mo[j] + (mb[j] - mo[j]) * ((double)nb / nn);
+  __syncthreads();  // mb / mo reads
+  for (int j = t; j < P; j += kThreads)
+    mu[j] = na == 0.0 ? mb[j] : mo[j] + (mb[j] - mo[j]) * ((double)p.adaptint / nn);
   if (t == 0) {
     st.wsum[c] = nn;
     fail = 0;
@@ -1516,48 +1594,52 @@ __global__ __launch_bounds__(kThreads) void k_adapt_mfma(DramState st, DramParam
   }
   __syncthreads();
   TCI_APHASE(2)
-  // ---- blocked Cholesky U'U of the tiles, in place (upper tiles become U)
-  for (int pk = 0; pk < NT; ++pk) {
-    double* D = Tl + ad_tile(pk, pk, NT) * 256;
-    // (1) the diagonal tile, by wave 0: 16 right-looking steps on LDS
-    if (w == 0) {
-      for (int k = 0; k < 16; ++k) {
-        const double d = D[k * 17];
-        if (!(d > 0.0) || !isfinite(d)) {
-          if (lane == 0) fail = 1;
-          break;  // uniform
-        }
-        const double rs = 1.0 / sqrt(d);
-        double ui[4], uj[4], dij[4];
+  // ---- blocked Cholesky U'U of the owned tiles; panel row pk goes through LDS buffer pk & 1
+  bool ok = true;
+  for (int pk = 0; pk < ((TCI_ADAPT_ABLATE & 1) ? 0 : NT); ++pk) {
+    double* B = Pb + (pk & 1) * NT * 256;  // tile (pk, tj) at B + 256 tj
+    double* D = B + 256 * pk;
+    // (1) row pk to LDS; the diagonal tile is factored in its owner's registers on the way
+    double dt[4] = {0.0, 0.0, 0.0, 0.0};
+    bool own_diag = false;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int e = lane + 64 * m, i = e >> 4, j = e & 15;
-          ui[m] = D[k * 16 + i];
-          uj[m] = D[k * 16 + j];
-          dij[m] = D[e];
-        }
+    for (int o = 0; o < kAdOwn; ++o) {
+      if (o >= nown || sti[o] != pk) continue;  // uniform
+      if (stj[o] == pk) {
+        own_diag = true;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int e = lane + 64 * m, i = e >> 4, j = e & 15;
-          if (i > k && j >= i) D[e] = dij[m] - (ui[m] * rs) * (uj[m] * rs);
-          else if (i == k && j >= k) D[e] = uj[m] * rs;
-        }
-        wave_sync();
+        for (int q = 0; q < 4; ++q) dt[q] = acc[o][q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) B[256 * stj[o] + (kq + 4 * q) * 16 + row] = acc[o][q];
       }
     }
+    if (own_diag) {  // uniform
+      bool bad = false;
+      chol16_step<0>(dt, lane, rdg, bad);
+      wave_sync();
+      chol16_finish(dt, lane, rdg, rdg);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) D[(kq + 4 * q) * 16 + row] = dt[q];
+      if (bad && lane == 0) fail = 1;
+    }
     __syncthreads();
-    if (fail) break;
-    // (2) the panel's row tiles (pk, tj > pk): U_pk' X = A -> X, one column per lane, 4 tiles per wave
+    TCI_APHASE(3)
+    if (fail) {
+      ok = false;
+      break;
+    }
+    // (2) the panel's row tiles (pk, tj > pk): U_pk' X = A -> X, one column per lane
     {
       const int g = w * 4 + kq;  // 16-lane group 0..15
       for (int tj = pk + 1 + g; tj < NT; tj += 16) {
-        double* A = Tl + ad_tile(pk, tj, NT) * 256;
+        double* A = B + 256 * tj;
         double x[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) x[k] = A[k * 16 + row];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-          x[k] = x[k] / D[k * 17];
+          x[k] = x[k] * rdg[k];
 #pragma unroll
           for (int m = k + 1; m < 16; ++m) x[m] = fma(-D[k * 16 + m], x[k], x[m]);
         }
@@ -1566,45 +1648,42 @@ __global__ __launch_bounds__(kThreads) void k_adapt_mfma(DramState st, DramParam
       }
     }
     __syncthreads();
-    // (3) trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj (rank-16, 4 MFMAs), every 4th per wave
-    {
-      const int m = NT - 1 - pk, TT = m * (m + 1) / 2;
-      int ti = pk + 1, tj = pk + 1;
-      for (int k = 0; k < TT; ++k) {
-        if ((k & 3) == w) {
-          double* C = Tl + ad_tile(ti, tj, NT) * 256;
-          const double* Xi = Tl + ad_tile(pk, ti, NT) * 256;
-          const double* Xj = Tl + ad_tile(pk, tj, NT) * 256;
-          f64x4 cacc;
+    TCI_APHASE(5)
+    // (3) the owners take row pk of U back; trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj
 #pragma unroll
-          for (int q = 0; q < 4; ++q) cacc[q] = C[(kq + 4 * q) * 16 + row];
+    for (int o = 0; o < kAdOwn; ++o) {
+      if (o >= nown) continue;  // uniform
+      if (sti[o] == pk) {
 #pragma unroll
-          for (int k4 = 0; k4 < 16; k4 += 4)
-            cacc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Xi[(k4 + kq) * 16 + row], Xj[(k4 + kq) * 16 + row], cacc, 0, 0, 0);
+        for (int q = 0; q < 4; ++q) acc[o][q] = B[256 * stj[o] + (kq + 4 * q) * 16 + row];
+      } else if (sti[o] > pk) {
+        const double* Xi = B + 256 * sti[o];
+        const double* Xj = B + 256 * stj[o];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) C[(kq + 4 * q) * 16 + row] = cacc[q];
-        }
-        if (++tj == NT) tj = ++ti;
+        for (int k4 = 0; k4 < 16; k4 += 4)
+          acc[o] = __builtin_amdgcn_mfma_f64_16x16x4f64(-Xi[(k4 + kq) * 16 + row], Xj[(k4 + kq) * 16 + row], acc[o], 0,
+                                                        0, 0);
       }
     }
-    __syncthreads();
+    TCI_APHASE(0)
   }
-  TCI_APHASE(3)
-  if (!fail) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
+  if (ok && !(TCI_ADAPT_ABLATE & 1)) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
-    const int il = t >> 4, jl = t & 15;  // one element of every upper tile per thread
-#pragma unroll 4
-    for (int ti = 0; ti < NT; ++ti)
-      for (int tj = ti; tj < NT; ++tj) {
-        const int i = 16 * ti + il, j = 16 * tj + jl;
-        if (i < P && j < P && j >= i) store_R(st, c, P, i, j, f32_round(Tl[ad_tile(ti, tj, NT) * 256 + t] * sc));
+#pragma unroll
+    for (int o = 0; o < kAdOwn; ++o) {
+      if (o >= nown) continue;  // uniform
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 16 * sti[o] + kq + 4 * q, j = 16 * stj[o] + row;
+        if (i < P && j < P && j >= i) store_R(st, c, P, i, j, f32_round(acc[o][q] * sc));
       }
+    }
   }
   __syncthreads();
   TCI_APHASE(4)
 #undef TCI_APHASE
   if (TCI_ADAPT_PROFILE && t == 0 && st.prof != nullptr)
-    for (int q = 0; q < 5; ++q) atomicAdd((unsigned long long*)&st.prof[q], (unsigned long long)aph[q]);
+    for (int q = 0; q < 6; ++q) atomicAdd((unsigned long long*)&st.prof[q], (unsigned long long)aph[q]);
   if (t == 0) st.nrej_win[c] = 0;
 }
 
