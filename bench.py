@@ -155,6 +155,91 @@ def end_to_end(lk, n_steps: int, seed: int, reduce=None):
             "accept_rate_median_rank0": float(np.median(fr.accept_rate))}
 
 
+def synthetic_kernel(cfg: int, rank: int, world: int, device_index: int, proposals: int, warmup: int, steps: int,
+                     reduce):
+    """SURVEY.md §8(d) configs 4/5 in kernel mode: 10,000 synthetic cells x 200 points, sharded
+    10,000/world cells per GPU (data seed 20201028 + rank), `proposals` Gaussian proposals per cell
+    around the ground truth with the reference's J0 variances (bounds-rejected rows inactive, not
+    counted). Config 5 runs the 2-segment, 3x-length construct. Strong scaling: the total is fixed."""
+    import torch
+
+    from transcriptioncycleinference_amd import Likelihood, from_lists
+    from transcriptioncycleinference_amd.construct import builtin_construct, long_two_loop_construct
+    from transcriptioncycleinference_amd.data import DR_BOUNDS, LOWER, UPPER, synthetic_cells
+
+    construct = builtin_construct(CONSTRUCT) if cfg == 4 else long_two_loop_construct()
+    n_total, n_points = 10000, 200
+    lo, hi = rank * n_total // world, (rank + 1) * n_total // world
+
+    def fwd(times, theta):
+        nan = [np.full(len(t), np.nan) for t in times]
+        tab = from_lists([(t, a, a) for t, a in zip(times, nan)])
+        with Likelihood(tab, construct, device=device_index) as L:
+            return L.forward(theta, np.arange(len(times), dtype=np.int32), grid="interp")
+
+    cells, truth = synthetic_cells(hi - lo, n_points, 20201028 + rank, fwd)
+    C, ld = truth.shape
+    rng = np.random.default_rng(7 + rank)
+    cid = np.repeat(np.arange(C, dtype=np.int32), proposals)
+    dtl = np.array([cells.cell(c)[0][-1] - cells.cell(c)[0][-2] for c in range(C)])
+    sd = np.sqrt(np.concatenate([np.tile([0.05, 0.1, 0.0, 1.0, 1.0, 0.05, 0.5], (C, 1)), np.full((C, ld - 7), 0.5)], 1))
+    sd[:, 2] = np.sqrt(dtl)
+    theta = truth[cid] + rng.normal(0.0, 1.0, (len(cid), ld)) * sd[cid]
+    active = np.all((theta[:, :7] >= LOWER) & (theta[:, :7] <= UPPER), axis=1)
+    active &= np.all((theta[:, 7:] >= DR_BOUNDS[0]) & (theta[:, 7:] <= DR_BOUNDS[1]), axis=1)
+    active = active.astype(np.uint8)
+    dev = torch.device("cuda", device_index)
+    lk = Likelihood(cells, construct, device=device_index)
+    th_d, cid_d = torch.from_numpy(theta).to(dev), torch.from_numpy(cid).to(dev)
+    act_d, out_d = torch.from_numpy(active).to(dev), torch.empty(len(cid), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(warmup):
+        lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=stream)
+    torch.cuda.synchronize(dev)
+    reduce(0.0, "max")  # barrier
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    elapsed = reduce(time.perf_counter() - t0, "max")
+    kernel_ms = e0.elapsed_time(e1) / steps
+    ss = out_d.cpu().numpy()
+    n_act = int(active.sum())
+    alg = algorithmic_bytes(cells, cid, active)
+    out = {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points, {proposals} proposals/cell, "
+                       f"construct {construct.name}, {hi - lo} cells on rank 0",
+           "value": reduce(n_act, "sum") * steps / elapsed, "unit": "SS evals/s", "scaling": "strong",
+           "kernel_ms_rank0": kernel_ms, "rows_per_launch_rank0": len(cid), "in_bounds_rank0": n_act,
+           "hbm_frac_rank0": alg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           "kernel_rows_per_lane": lk.info["rows_per_lane"],
+           "results_finite": bool(np.all(np.isfinite(ss[active.astype(bool)])))}
+    lk.close()
+    return out
+
+
+def hierarchical_end_to_end(lk, n_steps: int, seed: int, reduce):
+    """the 299-cell fit with loadPrevious, v fixed to v0 +- 1e-5 (proposal
+    variance 1e-7, TranscriptionCycleMCMC.m:218,236-237), v0 = the reference's MCMCresults.mean_v
+    (28-Oct-2020-TestData.mat, committed in tests/golden/forward_means.npz)."""
+    from transcriptioncycleinference_amd.mcmc import fit
+
+    with np.load(os.path.join(ROOT, "tests", "golden", "forward_means.npz"), allow_pickle=False) as f:
+        th, off = f["theta"], f["theta_offsets"]
+    v0 = [float(th[off[c]]) for c in range(len(off) - 1)]
+    t0 = time.perf_counter()
+    fr = fit(lk, n_steps=n_steps, n_burn=max(1, n_steps // 20), seed=seed, v0=v0)
+    wall = reduce(time.perf_counter() - t0, "max")
+    dev_s, evals = reduce(fr.elapsed_ms * 1e-3, "max"), int(reduce(fr.n_evals, "sum"))
+    return {"n_steps": n_steps, "chains": int(reduce(len(fr.MCMCresults), "sum")), "device_s": dev_s, "wall_s": wall,
+            "ssfun_evals": evals, "value": evals / dev_s, "unit": "SS evals/s",
+            "us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
+            "v_fixed": bool(all(abs(r["mean_v"] - v0[int(r["cell_index"]) - 1]) <= 1e-5 + 1e-12
+                                for r in fr.MCMCresults))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,6 +250,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dram-steps", type=int, default=200000,
                     help="end-to-end mode: one DRAM chain per TestData cell for this many steps (0 = skip)")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the other BASELINE configs (3: hierarchical fit; 4/5: 10k synthetic cells, kernel mode)")
     args = ap.parse_args()
 
     import torch
@@ -306,6 +393,19 @@ def main():
         if distributed:
             dist.barrier()
         res["end_to_end_dram"] = end_to_end(lk, args.dram_steps, seed=1 + rank, reduce=reduce)
+        if not args.no_configs:
+            res["config3_hierarchical_dram"] = hierarchical_end_to_end(lk, args.dram_steps, seed=3 + rank, reduce=reduce)
+    if not args.no_configs:
+        def reduce_k(x, op):
+            if not distributed:
+                return x
+            t = torch.tensor([float(x)], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+            return float(t.item())
+
+        for cfg in (4, 5):
+            res[f"config{cfg}_kernel"] = synthetic_kernel(cfg, rank, world, device_index, 8, args.warmup, args.steps,
+                                                          reduce_k)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cells, theta, cid, active, args.cpu_seconds)
     if rank == 0:
