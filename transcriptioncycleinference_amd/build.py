@@ -39,7 +39,10 @@ def build_library(force: bool = False, verbose: bool = False, out: str = LIB, de
     """Compile libtci.so (or an A/B variant with extra -D defines into `out`)."""
     if out == LIB and not defines and not force and not needs_rebuild():
         return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
+    # -amdgpu-mfma-vgpr-form: MFMA accumulators in VGPRs (the AGPR form made the compiler copy every
+    # accumulator into AGPRs and back around each f64 MFMA of the draws pass and wait for it)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-mllvm", "-amdgpu-mfma-vgpr-form",
+           "-fPIC", "-shared",
            "-Wall", "-Wno-bitwise-instead-of-logical", "-Wno-pass-failed", "-I" + os.path.join(REPO_ROOT, "include"), "-I" + CSRC,
            *[f"-D{d}" for d in (defines or [])], *SOURCES, "-o", out + ".tmp"]
     if verbose:

@@ -227,38 +227,42 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
   const int row = lane & 15, kq = lane >> 4;
   const int ntiles = (P + 15) >> 4;
   int nt[CT], kmx[CT];
-  int kend = -1;
 #pragma unroll
   for (int g = 0; g < CT; ++g) {
     nt[g] = ntiles - 1 - (4 * g + ((g & 1) ? 3 - w : w));  // uniform: costliest tiles first, snake order
     kmx[g] = nt[g] >= 0 ? min(16 * nt[g] + 15, P - 1) : -1;
-    kend = max(kend, kmx[g]);
   }
+  // The tiles are in decreasing k-extent (kmx[0] >= kmx[1] >= ..), so the k-steps split into
+  // phases with a compile-time number ng of active tiles: every inner loop is branch-free (the
+  // accumulators stay in place) and runs ng*MT independent MFMA chains.
   f64x4 acc[CT][MT];
 #pragma unroll
   for (int g = 0; g < CT; ++g)
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[g][m] = f64x4{0.0, 0.0, 0.0, 0.0};
-  for (int i0 = 0; i0 <= kend; i0 += 4) {
-    const int i = i0 + kq;
-    const int ic = i < P ? i : P - 1;
-    double a[MT];
+  int i0 = 0;
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int r = 16 * m + row;
-      const double zv = Z[(r < M ? r : M - 1) * zs + ic];  // clamped: rows >= M read row M-1, zeroed
-      a[m] = (r < M && i < P) ? zv : 0.0;
-    }
-    const int toff = tri_off(ic, P) - ic;
+  for (int ng = CT; ng >= 1; --ng) {
+    for (; i0 <= kmx[ng - 1]; i0 += 4) {  // tiles g < ng still need k-step i0
+      const int i = i0 + kq;
+      const int ic = i < P ? i : P - 1;
+      double a[MT];
 #pragma unroll
-    for (int g = 0; g < CT; ++g) {
-      if (i0 > kmx[g]) continue;  // uniform (invalid tiles: kmx = -1)
-      const int j = 16 * nt[g] + row;
-      const int jc = j < P ? j : P - 1;
-      const float rv = Rl[toff + (jc >= ic ? jc : ic)];
-      const double b = (i <= j && j < P) ? (double)rv : 0.0;
+      for (int m = 0; m < MT; ++m) {
+        const int r = 16 * m + row;
+        const double zv = Z[(r < M ? r : M - 1) * zs + ic];  // clamped: rows >= M read row M-1, zeroed
+        a[m] = (r < M && i < P) ? zv : 0.0;
+      }
+      const int toff = tri_off(ic, P) - ic;
 #pragma unroll
-      for (int m = 0; m < MT; ++m) acc[g][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b, acc[g][m], 0, 0, 0);
+      for (int g = 0; g < ng; ++g) {
+        const int j = 16 * nt[g] + row;
+        const int jc = j < P ? j : P - 1;
+        const float rv = Rl[toff + (jc >= ic ? jc : ic)];
+        const double b = (i <= j && j < P) ? (double)rv : 0.0;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[g][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b, acc[g][m], 0, 0, 0);
+      }
     }
   }
 #pragma unroll
