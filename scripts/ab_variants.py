@@ -26,6 +26,10 @@ VARIANTS = {
     "loopramp": ["TCI_RAMP_PREFIX=0"],
     "abl_loads": ["TCI_ABLATE=16"],
     "chainprof": ["TCI_CHAIN_PROFILE=1"],
+    "chainprof2": ["TCI_CHAIN_PROFILE=2"],
+    "rec2_s3": ["TCI_REC_WAVE=2", "TCI_S2_WAVE=3"],
+    "rec2_s2": ["TCI_REC_WAVE=2", "TCI_S2_WAVE=2"],
+    "rec3_s2": ["TCI_REC_WAVE=3", "TCI_S2_WAVE=2"],
     "adaptprof": ["TCI_ADAPT_PROFILE=1"],
     "adapt_twice": ["TCI_ADAPT_TWICE=1"],
     "adapt_nochol": ["TCI_ADAPT_ABLATE=1"],

@@ -853,6 +853,16 @@ __device__ __forceinline__ uint64_t stamp() {
 #endif
 }
 
+// Which waves keep the chain records (window row + column sums + posterior Welford, and the s2
+// statistics): waves that finish their evaluations early have slack before the barrier.
+#ifndef TCI_REC_WAVE
+#define TCI_REC_WAVE 0
+#endif
+#ifndef TCI_S2_WAVE
+#define TCI_S2_WAVE 1
+#endif
+constexpr int kRecWave = TCI_REC_WAVE, kS2Wave = TCI_S2_WAVE;
+
 template <int RPL, int NSEG>
 __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
                                                     int64_t s_end) {
@@ -891,7 +901,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     mu[k] = in ? st.pmu[c * ld + j] : 0.0;
     sg[k] = in ? st.psig[c * ld + j] : 0.0;
     smn[k] = sm2[k] = wsv[k] = 0.0;
-    if (w == 0 && in) {  // wave 0 keeps the posterior Welford statistics and the window sums
+    if (w == kRecWave && in) {  // the record wave keeps the posterior Welford statistics and window sums
       smn[k] = st.smean[c * ld + j];
       sm2[k] = st.sm2[c * ld + j];
       wsv[k] = st.wsumv[c * ld + j];
@@ -912,7 +922,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   }
   double ss = st.ss[c], prior = st.prior[c], s2 = st.sigma2[c];
   S2Stats s2a{0.0, 0.0, 0.0};  // held by wave 1
-  if (w == 1) s2a = S2Stats{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
+  if (w == kS2Wave) s2a = S2Stats{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
   int32_t nacc = st.naccept[c], nrej = st.nrej_win[c];
   int64_t nev = st.nevals[c];
   // this wave's proposal offsets: rows s + ahead (cur), s + ahead + 1, s + ahead + 2 (prefetched)
@@ -1045,8 +1055,8 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       if (p.updatesigma) s2 = hh ? (acc ? s2_4 : acc2 ? s2_5 : s2_3) : (acc ? s2_1 : acc2 ? s2_2 : s2_0);
       // the row's records
       const int64_t row = s + hh;
-      if (w == 0) record_vec_reg<NJ>(st, p, c, row, P, th, smn, sm2, wsv, lane, cur);
-      if (w == 1 && lane == 0) record_s2_cur(st, p, c, row, s2, s2a, cur);
+      if (w == kRecWave) record_vec_reg<NJ>(st, p, c, row, P, th, smn, sm2, wsv, lane, cur);
+      if (w == kS2Wave && lane == 0) record_s2_cur(st, p, c, row, s2, s2a, cur);
       cur.next(p);
       adv = hh + 1;
       if (moved) break;  // step s+1 must be re-proposed around the new state
@@ -1071,9 +1081,16 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     if (TCI_CHAIN_PROFILE) ph[5] += 1ull << 40;  // round count in the high bits
   }
 #undef TCI_PHASE
+#if TCI_CHAIN_PROFILE == 2  // per wave: barrier wait (slot w) and eval + prior + exchange (slot 4 + w)
+  if (lane == 0 && st.prof != nullptr) {
+    atomicAdd((unsigned long long*)&st.prof[w], (unsigned long long)ph[3]);
+    atomicAdd((unsigned long long*)&st.prof[4 + w], (unsigned long long)(ph[1] + ph[2]));
+  }
+#else
   if (TCI_CHAIN_PROFILE && w == 0 && lane == 0 && st.prof != nullptr)
     for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long*)&st.prof[k], (unsigned long long)ph[k]);
-  if (w == 0) {
+#endif
+  if (w == kRecWave) {
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
       const int j = lane + 64 * k;
@@ -1093,7 +1110,8 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       st.nevals[c] = nev;
       if (c == 0) *st.step = s_end;  // k_adapt reads the row it follows
     }
-  } else if (w == 1 && lane == 0) {
+  }
+  if (w == kS2Wave && lane == 0) {
     st.s2sum[c] = s2a.sum;
     st.sq_mean[c] = s2a.qmean;
     st.sq_m2[c] = s2a.qm2;
