@@ -30,6 +30,7 @@ VARIANTS = {
     "rec2_s3": ["TCI_REC_WAVE=2", "TCI_S2_WAVE=3"],
     "rec2_s2": ["TCI_REC_WAVE=2", "TCI_S2_WAVE=2"],
     "rec3_s2": ["TCI_REC_WAVE=3", "TCI_S2_WAVE=2"],
+    "normal_f32": ["TCI_NORMAL_F32=1"],
     "adaptprof": ["TCI_ADAPT_PROFILE=1"],
     "adapt_twice": ["TCI_ADAPT_TWICE=1"],
     "adapt_nochol": ["TCI_ADAPT_ABLATE=1"],
