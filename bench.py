@@ -155,17 +155,12 @@ def end_to_end(lk, n_steps: int, seed: int, reduce=None):
             "accept_rate_median_rank0": float(np.median(fr.accept_rate))}
 
 
-def synthetic_kernel(cfg: int, rank: int, world: int, device_index: int, proposals: int, warmup: int, steps: int,
-                     reduce):
-    """SURVEY.md §8(d) configs 4/5 in kernel mode: 10,000 synthetic cells x 200 points, sharded
-    10,000/world cells per GPU (data seed 20201028 + rank), `proposals` Gaussian proposals per cell
-    around the ground truth with the reference's J0 variances (bounds-rejected rows inactive, not
-    counted). Config 5 runs the 2-segment, 3x-length construct. Strong scaling: the total is fixed."""
-    import torch
-
+def synthetic_config_cells(cfg: int, rank: int, world: int, device_index: int):
+    """this rank's shard of the 10,000 synthetic cells x 200 points
+    (data seed 20201028 + rank) and the construct (config 5: 2 segments per dye, 3x length)."""
     from transcriptioncycleinference_amd import Likelihood, from_lists
     from transcriptioncycleinference_amd.construct import builtin_construct, long_two_loop_construct
-    from transcriptioncycleinference_amd.data import DR_BOUNDS, LOWER, UPPER, synthetic_cells
+    from transcriptioncycleinference_amd.data import synthetic_cells
 
     construct = builtin_construct(CONSTRUCT) if cfg == 4 else long_two_loop_construct()
     n_total, n_points = 10000, 200
@@ -178,6 +173,21 @@ def synthetic_kernel(cfg: int, rank: int, world: int, device_index: int, proposa
             return L.forward(theta, np.arange(len(times), dtype=np.int32), grid="interp")
 
     cells, truth = synthetic_cells(hi - lo, n_points, 20201028 + rank, fwd)
+    return cells, truth, construct, n_total, n_points, lo, hi
+
+
+def synthetic_kernel(cfg: int, rank: int, world: int, device_index: int, proposals: int, warmup: int, steps: int,
+                     reduce):
+    """SURVEY.md §8(d) configs 4/5 in kernel mode: 10,000 synthetic cells x 200 points, sharded
+    10,000/world cells per GPU (data seed 20201028 + rank), `proposals` Gaussian proposals per cell
+    around the ground truth with the reference's J0 variances (bounds-rejected rows inactive, not
+    counted). Config 5 runs the 2-segment, 3x-length construct. Strong scaling: the total is fixed."""
+    import torch
+
+    from transcriptioncycleinference_amd import Likelihood
+    from transcriptioncycleinference_amd.data import DR_BOUNDS, LOWER, UPPER
+
+    cells, truth, construct, n_total, n_points, lo, hi = synthetic_config_cells(cfg, rank, world, device_index)
     C, ld = truth.shape
     rng = np.random.default_rng(7 + rank)
     cid = np.repeat(np.arange(C, dtype=np.int32), proposals)
@@ -218,6 +228,31 @@ def synthetic_kernel(cfg: int, rank: int, world: int, device_index: int, proposa
            "results_finite": bool(np.all(np.isfinite(ss[active.astype(bool)])))}
     lk.close()
     return out
+
+
+def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_steps: int, reduce,
+                         engine: str = "auto"):
+    """SURVEY.md §8(d) configs 4/5 end to end: this rank's shard of the 10,000 synthetic cells
+    fitted by the GPU-resident DRAM (one chain per cell, n_burn = n_steps/20), as
+    `parallel.fit_sharded` runs it minus the results gather. Strong scaling: 10,000 cells in total.
+    n_steps is a bounded sample of the reference's 200k (the per-step cost is constant once the
+    first adaptation has run; stated in the output)."""
+    from transcriptioncycleinference_amd import Likelihood
+    from transcriptioncycleinference_amd.mcmc import DramOptions, fit
+
+    cells, _, construct, n_total, n_points, lo, hi = synthetic_config_cells(cfg, rank, world, device_index)
+    with Likelihood(cells, construct, device=device_index) as lk:
+        reduce(0.0, "max")  # barrier
+        t0 = time.perf_counter()
+        fr = fit(lk, n_steps=n_steps, n_burn=max(1, n_steps // 20), seed=cfg, opts=DramOptions(engine=engine))
+        wall = reduce(time.perf_counter() - t0, "max")
+    dev_s, evals = reduce(fr.elapsed_ms * 1e-3, "max"), int(reduce(fr.n_evals, "sum"))
+    return {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points, construct {construct.name}, "
+                        f"{hi - lo} chains on rank 0, {n_steps} steps (bounded sample of 200k)",
+            "n_steps": n_steps, "engine": engine, "chains": int(reduce(len(fr.MCMCresults), "sum")), "device_s": dev_s,
+            "wall_s": wall, "ssfun_evals": evals, "value": evals / dev_s, "unit": "SS evals/s", "scaling": "strong",
+            "us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
+            "accept_rate_median_rank0": float(np.median(fr.accept_rate))}
 
 
 def hierarchical_end_to_end(lk, n_steps: int, seed: int, reduce):

@@ -161,8 +161,7 @@ typedef struct {
  *            the loop (one workgroup barrier per step): latency-bound runs (few chains).
  *   BATCHED: one launch per stage, every chain's ssfun in the batched likelihood kernel, replayed
  *            as a hipGraph per adaptation window: many chains, or cells too long for FUSED.
- *   AUTO:    FUSED when its draws pass fits a CU's LDS (P <= ~225) and there are at most 8 chains
- *            per CU. */
+ *   AUTO:    FUSED whenever its draws pass fits a CU's LDS (P <= ~225); BATCHED otherwise. */
 #define TCI_DRAM_AUTO 0
 #define TCI_DRAM_FUSED 1
 #define TCI_DRAM_BATCHED 2

@@ -16,6 +16,7 @@ OUT = os.path.join(ROOT, "build", "ab")
 
 VARIANTS = {
     "ship": [],
+    "old": None,  # a prebuilt library of the previous commit, copied to build/ab/libtci_old.so
     "abl_rows": ["TCI_ABLATE=1"],
     "abl_bounds": ["TCI_ABLATE=2"],
     "abl_interp": ["TCI_ABLATE=4"],
@@ -86,7 +87,12 @@ def run(names, rounds, launches, proposals):
     res = {}
     for n in names:
         got = outs[n].cpu().numpy()
-        rel = float(np.nanmax(np.abs(got[act] - ref[act]) / np.abs(ref[act])))
+        rr = np.abs(got - ref) / np.abs(ref)
+        rr[~act] = 0
+        rel = float(np.nanmax(rr))
+        bad = np.nonzero(~(rr <= 1e-12))[0]
+        if len(bad):
+            print(n, "mismatching rows", len(bad), "first", [(int(i), int(cid[i]), float(ref[i]), float(got[i])) for i in bad[:8]], file=sys.stderr)
         t = np.array(times[n])
         res[n] = {"median_us": float(np.median(t)), "min_us": float(t.min()), "rel_vs_first": rel,
                   "evals_per_s": float(act.sum() / (np.median(t) * 1e-6)), "defines": VARIANTS.get(n)}

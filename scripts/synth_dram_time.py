@@ -1,0 +1,15 @@
+#!/usr/bin/env python3
+"""Time the GPU-resident DRAM fit of BASELINE configs 4/5 (10,000 synthetic cells x 200 points) on
+one GPU:  python scripts/synth_dram_time.py CFG STEPS [CFG STEPS ...]   (TCI_ENGINE=auto|fused|batched)"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+args = sys.argv[1:]
+for i in range(0, len(args), 2):
+    cfg, steps = int(args[i]), int(args[i + 1])
+    print(json.dumps(bench.synthetic_end_to_end(cfg, 0, 1, 0, steps, reduce=lambda x, op: x,
+                                                    engine=os.environ.get("TCI_ENGINE", "auto"))), flush=True)

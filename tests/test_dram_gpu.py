@@ -360,3 +360,49 @@ def test_sharded_fit_world2_equals_the_one_gpu_fit(lk):
     want = pack_results(fit(lk, n_steps=400, n_burn=150, seed=4), int(lk.cells.lengths.max()))
     assert got.shape == want.shape == (299, want.shape[1])
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.fixture(scope="module")
+def lk_long():
+    """Synthetic cells of 150 and 200 points (P = 157, 207): the adaptation runs on the 8-wave
+    matrix-core kernel (k_adapt_mfma<8, 13>, P <= 208), as for BASELINE configs 4/5."""
+    from transcriptioncycleinference_amd import Likelihood, from_lists
+
+    rng = np.random.default_rng(11)
+    cells = []
+    for k in range(12):
+        n = 200 if k % 3 else 150
+        t = 0.2454 * np.arange(n) + rng.uniform(-0.012, 0.012, n)
+        ms2 = rng.normal(20.0, 5.0, n)
+        pp7 = rng.normal(10.0, 3.0, n)
+        ms2[rng.random(n) < 0.37] = np.nan
+        cells.append((t, ms2, pp7))
+    with Likelihood(from_lists(cells), "P2P-MS2v5-LacZ-PP7v4", device=0) as L:
+        yield L
+
+
+@pytest.mark.parametrize("engine", ["fused", "batched"])
+def test_long_cells_adapted_proposal_is_the_scaled_chain_covariance(lk_long, engine):
+    """As test_adapted_proposal_is_the_scaled_chain_covariance, for P in (144, 208] (the 8-wave
+    adaptation kernel); the fused and batched engines agree bitwise."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions, dram_run
+
+    ids = list(range(12))
+    o = DramOptions(n_steps=500, burnintime=200, adaptint=100, stats_from=1, thin=1, seed=4, engine=engine)
+    x0, lo, hi, mu, sg, J0 = setup_rows(lk_long.cells, ids, 0)
+    res = dram_run(lk_long, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, want_qcov=True)
+    n = lk_long.cells.lengths[ids]
+    for k in range(len(ids)):
+        P = 7 + int(n[k])
+        X = res.chain[:500, k, :P]
+        C = np.cov(X.T, ddof=1) + 1e-5 * np.eye(P)
+        R = res.qcov_R[k, :P, :P]
+        assert np.all(np.tril(R, -1) == 0)
+        assert np.array_equal(R, R.astype(np.float32).astype(np.float64))
+        want = (2.4 ** 2 / P) * C
+        np.testing.assert_allclose(R.T @ R, want, rtol=1e-6, atol=1e-6 * np.abs(want).max())
+    if engine == "batched":
+        o.engine = "fused"
+        res_f = dram_run(lk_long, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, want_qcov=True)
+        np.testing.assert_array_equal(res_f.chain, res.chain)
+        np.testing.assert_array_equal(res_f.qcov_R, res.qcov_R)

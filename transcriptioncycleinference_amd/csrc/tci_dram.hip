@@ -1461,9 +1461,9 @@ __device__ __forceinline__ void chol16_finish(double (&a)[4], int lane, double* 
   }
 }
 
-// ---- Adaptation on matrix cores, for P <= 16 * kAdM (every TestData cell). One workgroup per
-// chain. The upper triangle of cov + qcovadj I is held as 16 x 16 tiles in the MFMA accumulator
-// layout, in REGISTERS: wave w owns every 4th tile of the row-major tile order for the whole
+// ---- Adaptation on matrix cores, for P <= 16 * MAXT (every TestData cell; configs 4/5). One
+// workgroup per chain. The upper triangle of cov + qcovadj I is held as 16 x 16 tiles in the MFMA
+// accumulator layout, in REGISTERS: wave w owns every NW-th tile of the row-major tile order for the
 // kernel. LDS holds only one batch of window rows (scatter) or, aliased onto it, two panel
 // buffers (Cholesky): ~39 KB, so two chains' workgroups share a CU and all 299 TestData chains are
 // resident at once (a 131 KB tile-in-LDS layout ran them in two rounds on 256 CUs).
@@ -1477,17 +1477,23 @@ __device__ __forceinline__ void chol16_finish(double (&a)[4], int lane, double* 
 //     tiles back and every trailing tile takes the rank-16 update as 4 MFMAs on its owner's
 //     registers. R = U * adascale, stored only when the
 //     whole factorization succeeded (a singular matrix keeps the previous R, as mcmcstat).
-constexpr int kAdM = 9;     // max tiles per dimension (P <= 144)
+// Instances: NW waves per workgroup (one chain), MAXT = max tiles per dimension, kAdOwn output tiles
+// per wave (MAXT (MAXT + 1) / 2 <= NW kAdOwn): <4, 9> for P <= 144 (two chains per CU), <8, 13>
+// for P <= 208 (configs 4/5: 200 points, P = 207; one chain per CU at 256 VGPRs per wave).
 constexpr int kAdRB = 16;   // window rows per LDS batch
-constexpr int kAdOwn = 12;  // output tiles per wave: kAdM (kAdM + 1) / 2 <= 4 kAdOwn
+constexpr int kAdOwn = 12;  // output tiles per wave (a multiple of the merge group kAdMG)
 __host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P) {
   const int64_t NT = (P + 15) / 16, LX = 16 * NT;
   const int64_t shared = kAdRB * LX > 2 * NT * 256 ? kAdRB * LX : 2 * NT * 256;  // X | panel buffers
   return (shared + 2 * LX) * 8;
 }
 
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_adapt_mfma(DramState st,
-                                                                                                 DramParams p) {
+template <int NW, int MAXT>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_adapt_mfma(DramState st,
+                                                                                              DramParams p) {
+  constexpr int kAdM = MAXT;
+  constexpr int NTH = 64 * NW;
+  static_assert(MAXT * (MAXT + 1) / 2 <= NW * kAdOwn, "owned tiles per wave");
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int fail;
   __shared__ double rdg[16];  // 1 / U[k][k] of the current diagonal tile
@@ -1513,17 +1519,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
 #define TCI_APHASE(k) \
   if (TCI_ADAPT_PROFILE) { a1 = stamp(); aph[k] += a1 - a0; a0 = a1; }
   // ---- batch mean from the window's column sums (kept by the engines as rows are recorded)
-  for (int j = t; j < LX; j += kThreads) {
+  for (int j = t; j < LX; j += NTH) {
     mb[j] = j < P ? st.wsumv[c * ld + j] / (double)p.adaptint : 0.0;
     mo[j] = j < P ? mu[j] : 0.0;
   }
-  // owned tiles (ti <= tj): every 4th of the row-major tile order, from w. Slots past the last
+  // owned tiles (ti <= tj): every NW-th of the row-major tile order, from w. Slots past the last
   // tile compute on tile (0, 0) and are discarded, so the code is straight-line and every array
   // index is a compile-time constant (the tiles stay in registers, no scratch memory).
   int sti[kAdOwn], stj[kAdOwn];
 #pragma unroll
   for (int o = 0; o < kAdOwn; ++o) {
-    int k = w + 4 * o, ti = 0;
+    int k = w + NW * o, ti = 0;
     if (k >= T) k = 0;
     while (k >= NT - ti) {  // uniform
       k -= NT - ti;
@@ -1532,18 +1538,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     sti[o] = ti;
     stj[o] = ti + k;
   }
-  const int nown = (T - w + 3) / 4;  // valid slots
+  const int nown = (T - w + NW - 1) / NW;  // valid slots
   // ---- scatter of the centred rows on MFMA; batch r0 + kAdRB is loaded while r0 is multiplied
   f64x4 acc[kAdOwn];
 #pragma unroll
   for (int o = 0; o < kAdOwn; ++o) acc[o] = f64x4{0.0, 0.0, 0.0, 0.0};
-  constexpr int kPer = (kAdRB * 16 * kAdM + kThreads - 1) / kThreads;
+  constexpr int kPer = (kAdRB * 16 * kAdM + NTH - 1) / NTH;
   double v[kPer];
   auto load_batch = [&](int r0) {
     const int n = min(kAdRB, nb - r0);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-      const int e = t + u * kThreads, r = e / LX, j = e - r * LX;
+      const int e = t + u * NTH, r = e / LX, j = e - r * LX;
       v[u] = (e < kAdRB * LX && r < n && j < P) ? win[(int64_t)(r0 + r) * ld + j] : 0.0;
     }
   };
@@ -1553,7 +1559,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     const int n = min(kAdRB, nb - r0);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
-      const int e = t + u * kThreads, r = e / LX, j = e - r * LX;
+      const int e = t + u * NTH, r = e / LX, j = e - r * LX;
       if (e < kAdRB * LX) X[e] = (r < n && j < P) ? v[u] - mb[j] : 0.0;
     }
     __syncthreads();
@@ -1620,7 +1626,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     }
   }
   __syncthreads();  // mb / mo reads
-  for (int j = t; j < P; j += kThreads)
+  for (int j = t; j < P; j += NTH)
     mu[j] = na == 0.0 ? mb[j] : mo[j] + (mb[j] - mo[j]) * ((double)p.adaptint / nn);
   if (t == 0) {
     st.wsum[c] = nn;
@@ -1634,7 +1640,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     else if (rate < 0.05) s = p.burnin_scale;
     if (s != 1.0) {
       double* R = st.R + c * ld * ld;
-      for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
+      for (int64_t e = t; e < (int64_t)P * P; e += NTH) {
         const int i = (int)(e / P), j = (int)(e % P);
         store_R(st, c, P, i, j, f32_round(R[(int64_t)i * ld + j] * s));
       }
@@ -1682,8 +1688,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     }
     // (2) the panel's row tiles (pk, tj > pk): U_pk' X = A -> X, one column per lane
     {
-      const int g = w * 4 + kq;  // 16-lane group 0..15
-      for (int tj = pk + 1 + g; tj < NT; tj += 16) {
+      const int g = w * 4 + kq;  // 16-lane group 0 .. 4 NW - 1
+      for (int tj = pk + 1 + g; tj < NT; tj += 4 * NW) {
         double* A = B + 256 * tj;
         double x[16];
 #pragma unroll
@@ -1750,6 +1756,20 @@ int launch_stage(void (*k)(DramState, DramParams), const DramState& st, const Dr
   return finish();
 }
 
+template <int NW, int MAXT>
+int launch_adapt_mfma(const DramState& st, const DramParams& p, void* stream) {
+  const size_t bytes = (size_t)adapt_mfma_lds_bytes(p.pmax);
+  auto k = k_adapt_mfma<NW, MAXT>;
+  if (bytes > 48 * 1024 &&
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
+    return TCI_EHIP;
+  hipLaunchKernelGGL(k, chain_grid(st.n_chains), dim3(64 * NW), bytes, (hipStream_t)stream, st, p);
+#ifdef TCI_ADAPT_TWICE  // diagnostics only (wrong results): a second, warm launch of the same kernel
+  hipLaunchKernelGGL(k, chain_grid(st.n_chains), dim3(64 * NW), bytes, (hipStream_t)stream, st, p);
+#endif
+  return finish();
+}
+
 }  // namespace
 
 int dram_launch_init(const DramState& st, const double* qcov_diag, const double* sigma2_0, void* stream) {
@@ -1770,17 +1790,8 @@ int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream) 
   return launch_stage(k_accept2, st, p, stream);
 }
 int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
-  if (p.pmax <= 16 * kAdM) {
-    const size_t bytes = (size_t)adapt_mfma_lds_bytes(p.pmax);
-    if (bytes > 48 * 1024 && hipFuncSetAttribute((const void*)k_adapt_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)bytes) != hipSuccess)
-      return TCI_EHIP;
-    hipLaunchKernelGGL(k_adapt_mfma, chain_grid(st.n_chains), dim3(kThreads), bytes, (hipStream_t)stream, st, p);
-#ifdef TCI_ADAPT_TWICE  // diagnostics only (wrong results): a second, warm launch of the same kernel
-    hipLaunchKernelGGL(k_adapt_mfma, chain_grid(st.n_chains), dim3(kThreads), bytes, (hipStream_t)stream, st, p);
-#endif
-    return finish();
-  }
+  if (p.pmax <= 16 * 9) return launch_adapt_mfma<4, 9>(st, p, stream);
+  if (p.pmax <= 16 * 13) return launch_adapt_mfma<8, 13>(st, p, stream);
   const int64_t ntile = (p.pmax + 3) / 4;
   if (ntile * (ntile + 1) / 2 <= (int64_t)kAdaptTiles * kThreads && adapt_tiles_lds_bytes(p.pmax) <= 78 * 1024) {
     const size_t bytes = (size_t)adapt_tiles_lds_bytes(p.pmax);
