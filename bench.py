@@ -286,7 +286,9 @@ def main():
     ap.add_argument("--dram-steps", type=int, default=200000,
                     help="end-to-end mode: one DRAM chain per TestData cell for this many steps (0 = skip)")
     ap.add_argument("--no-configs", action="store_true",
-                    help="skip the other BASELINE configs (3: hierarchical fit; 4/5: 10k synthetic cells, kernel mode)")
+                    help="skip the other BASELINE configs (3: hierarchical fit; 4/5: 10k synthetic cells)")
+    ap.add_argument("--synth-dram-steps", type=int, default=2000,
+                    help="configs 4/5 end to end: DRAM steps of the 10,000-chain fit (a bounded sample of 200k; 0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -441,6 +443,9 @@ def main():
         for cfg in (4, 5):
             res[f"config{cfg}_kernel"] = synthetic_kernel(cfg, rank, world, device_index, 8, args.warmup, args.steps,
                                                           reduce_k)
+            if args.synth_dram_steps > 1:
+                res[f"config{cfg}_dram"] = synthetic_end_to_end(cfg, rank, world, device_index, args.synth_dram_steps,
+                                                                reduce_k)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cells, theta, cid, active, args.cpu_seconds)
     if rank == 0:
