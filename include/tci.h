@@ -147,24 +147,28 @@ typedef struct {
   int64_t stats_from;   /* first chain row (1-based) of the posterior summaries (n_burn, :276) */
   int64_t thin;         /* keep every thin-th chain row in outputs.chain (0 = keep none) */
   uint64_t seed;
-  int32_t engine;       /* TCI_DRAM_AUTO / TCI_DRAM_FUSED / TCI_DRAM_BATCHED (below) */
+  int32_t engine;       /* TCI_DRAM_AUTO / _FUSED / _BATCHED / _WALK (below) */
   int32_t reserved;
   const int64_t* chain_keys; /* optional [n_chains]: chain c draws from RNG stream chain_keys[c]
                                 (NULL: stream c). Keying chains by their global cell index makes a
                                 shard of a run (its cells on one GPU) reproduce the unsharded chains */
 } tci_dram_options;
 
-/* DRAM engines; both give identical chains for the same seed.
+/* DRAM engines; all give identical chains for the same seed.
  *   FUSED:   per chunk of steps (up to the next adaptation) one wide launch draws every
  *            state-independent random quantity (proposal offsets z*R on MFMA, uniforms, Gamma
  *            variates), then one workgroup per chain walks the chunk with its ssfun evaluations in
  *            the loop (one workgroup barrier per step): latency-bound runs (few chains).
  *   BATCHED: one launch per stage, every chain's ssfun in the batched likelihood kernel, replayed
  *            as a hipGraph per adaptation window: many chains, or cells too long for FUSED.
- *   AUTO:    FUSED whenever its draws pass fits a CU's LDS (P <= ~225); BATCHED otherwise. */
+ *   WALK:    FUSED's draws pass, then ONE WAVEFRONT per chain walks the chunk (stage 2 evaluated
+ *            only after a stage-1 rejection, no workgroup barriers): many chains (configs 4/5).
+ *   AUTO:    FUSED whenever its draws pass fits a CU's LDS (P <= ~225), as WALK beyond two chains
+ *            per CU; BATCHED otherwise. */
 #define TCI_DRAM_AUTO 0
 #define TCI_DRAM_FUSED 1
 #define TCI_DRAM_BATCHED 2
+#define TCI_DRAM_WALK 3
 
 /* Host buffers filled by tci_dram_run (any may be NULL). Per-chain vectors have stride ld. */
 typedef struct {

@@ -256,8 +256,11 @@ def test_fused_and_batched_engines_give_identical_chains(lk, ntry):
     a, _ = run(lk, ids, o)
     o.engine = "batched"
     b, _ = run(lk, ids, o)
+    o.engine = "walk"  # one wavefront per chain
+    c, _ = run(lk, ids, o)
     for f in ("chain", "s2chain", "mean", "std", "final_theta", "sigma_mean", "sigma_std", "accept_rate", "n_evals"):
         np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+        np.testing.assert_array_equal(getattr(c, f), getattr(b, f), err_msg="walk " + f)
     assert np.median(a.accept_rate) > 0.01
 
 
@@ -288,7 +291,7 @@ def test_adapted_proposal_is_the_scaled_chain_covariance(lk, engine):
         np.testing.assert_allclose(Q, want, rtol=1e-6, atol=1e-6 * np.abs(want).max())
 
 
-@pytest.mark.parametrize("engine", ["fused", "batched"])
+@pytest.mark.parametrize("engine", ["fused", "batched", "walk"])
 def test_chain_keys_let_a_shard_reproduce_the_full_run(lk, engine):
     """chains keyed by their global index reproduce, on a shard (a subset of the
     chains run alone, as one GPU of a sharded fit would), the rows of the unsharded run bitwise."""
@@ -402,7 +405,8 @@ def test_long_cells_adapted_proposal_is_the_scaled_chain_covariance(lk_long, eng
         want = (2.4 ** 2 / P) * C
         np.testing.assert_allclose(R.T @ R, want, rtol=1e-6, atol=1e-6 * np.abs(want).max())
     if engine == "batched":
-        o.engine = "fused"
-        res_f = dram_run(lk_long, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, want_qcov=True)
-        np.testing.assert_array_equal(res_f.chain, res.chain)
-        np.testing.assert_array_equal(res_f.qcov_R, res.qcov_R)
+        for other in ("fused", "walk"):
+            o.engine = other
+            res_f = dram_run(lk_long, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, want_qcov=True)
+            np.testing.assert_array_equal(res_f.chain, res.chain, err_msg=other)
+            np.testing.assert_array_equal(res_f.qcov_R, res.qcov_R, err_msg=other)

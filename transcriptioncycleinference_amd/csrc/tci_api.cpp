@@ -519,9 +519,9 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
       !qcov_diag || !sigma2_0)
     return fail(ctx, TCI_EINVAL, "tci_dram_run: null argument or no chains");
   if (opt->n_steps < 1 || opt->ntry < 1 || opt->ntry > 2 || opt->adaptint < 0 || !(opt->drscale > 0) ||
-      opt->engine < TCI_DRAM_AUTO || opt->engine > TCI_DRAM_BATCHED)
+      opt->engine < TCI_DRAM_AUTO || opt->engine > TCI_DRAM_WALK)
     return fail(ctx, TCI_EINVAL,
-                "tci_dram_run: bad options (n_steps >= 1, ntry in {1,2}, adaptint >= 0, engine in {0,1,2})");
+                "tci_dram_run: bad options (n_steps >= 1, ntry in {1,2}, adaptint >= 0, engine in {0,1,2,3})");
   int rc = check_rows(ctx, ld, cell_id, n_chains);
   if (rc != TCI_OK) return rc;
   if (ld > TCI_MAX_POINTS + 7) return fail(ctx, TCI_ERANGE, "tci_dram_run: ld too large");
@@ -667,9 +667,16 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   const bool fused_fits = fused_lds <= 160 * 1024;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
-  bool fused = opt->engine == TCI_DRAM_FUSED;
-  if (opt->engine == TCI_DRAM_AUTO)
+  // WALK (one wavefront per chain) once k_chain's one-workgroup-per-chain layout would need more
+  // than one round of resident workgroups (two chains per CU).
+  int n_cu = 0;
+  TCI_HIP(ctx, hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  bool fused = opt->engine == TCI_DRAM_FUSED || opt->engine == TCI_DRAM_WALK;
+  p.walk = opt->engine == TCI_DRAM_WALK ? 1 : 0;
+  if (opt->engine == TCI_DRAM_AUTO) {
     fused = fused_fits;
+    p.walk = n_chains > 2 * (int64_t)std::max(n_cu, 1) ? 1 : 0;
+  }
   if (fused && !fused_fits) return fail(ctx, TCI_ERANGE, "tci_dram_run: rows too long for the fused engine");
   if (fused) {
     // Chunks of chain rows up to the next adaptation row (and at most p.chunk rows: the draws

@@ -1147,6 +1147,174 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   }
 }
 
+// One wavefront per chain (the WALK engine: many chains, e.g. configs 4/5's 10,000): the same
+// chunk of rows as k_chain, step by step, stage 2 evaluated only when stage 1 is rejected. No
+// workgroup barriers; 4 chains per 256-thread workgroup, so a CU holds 4x the chains k_chain's
+// one-workgroup-per-chain layout does. Every value is computed by the same expressions as
+// k_chain (its step-s lanes) and the batched engine: identical chains (tests/test_dram_gpu.py).
+#ifndef TCI_WALK_WAVES
+#define TCI_WALK_WAVES 0  // > 0: amdgpu_waves_per_eu register budget for k_walk (A/B)
+#endif
+#if TCI_WALK_WAVES > 0
+#define TCI_WALK_OCC __attribute__((amdgpu_waves_per_eu(TCI_WALK_WAVES)))
+#else
+#define TCI_WALK_OCC
+#endif
+template <int RPL, int NSEG>
+__global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, DramParams p, KParams kp, int64_t s_begin,
+                                                                int64_t s_end) {
+  constexpr int NJ = RPL + 1;
+  constexpr int EV = eval_lds_doubles<RPL>();
+  constexpr int NW = kThreads / 64;
+  __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each wave's {K,J} tables / rows
+  __shared__ double yl[NW][64 * NJ];                            // each wave's proposal (theta broadcast)
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * NW + w;
+  if (c >= st.n_chains) return;  // uniform per wave; no workgroup barriers below
+  const int64_t ld = st.ld;
+  const int P = st.npar[c];
+  const int64_t DW = draw_stride(ld);
+  const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
+  const double inv_ds = 1.0 / p.drscale;
+  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], smn[NJ], sm2[NJ], wsv[NJ];
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    const int j = lane + 64 * k;
+    const bool in = j < P;
+    th[k] = in ? st.theta[c * ld + j] : 0.0;
+    lo[k] = in ? st.lower[c * ld + j] : 0.0;
+    hi[k] = in ? st.upper[c * ld + j] : 0.0;
+    mu[k] = in ? st.pmu[c * ld + j] : 0.0;
+    sg[k] = in ? st.psig[c * ld + j] : 0.0;
+    smn[k] = in ? st.smean[c * ld + j] : 0.0;
+    sm2[k] = in ? st.sm2[c * ld + j] : 0.0;
+    wsv[k] = in ? st.wsumv[c * ld + j] : 0.0;
+  }
+  EvalIn<RPL> e;  // the chain's cell records stay in registers
+  {
+    const int cell = st.cell[c];
+    const int64_t cbase = (int64_t)cell * kp.cell_stride;
+    e.cm = kp.cells[cell];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) e.st[q] = kp.steps[cbase + RPL * lane + q];
+#pragma unroll
+    for (int k = 0; k <= RPL; ++k) {
+      const int j = lane + 64 * k;
+      e.pt[k] = j <= 64 * RPL ? kp.points[cbase + j] : PointRec{NAN, NAN, NAN, 0, 0};
+    }
+  }
+  double ss = st.ss[c], prior = st.prior[c], s2 = st.sigma2[c];
+  S2Stats s2a{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
+  int32_t nacc = st.naccept[c], nrej = st.nrej_win[c];
+  int64_t nev = st.nevals[c];
+  double* yb = yl[w];
+  // ssfun and prior of the proposal th + scale * u (k_chain's per-wave evaluation)
+  auto evaluate = [&](const double* u, double scale, double* y, double& r, double& pr) {
+    bool out = false;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      y[k] = th[k] + scale * u[k];
+      if (lane + 64 * k < P) out |= !(y[k] >= lo[k] && y[k] <= hi[k]);
+    }
+    r = INFINITY;
+    pr = 0.0;
+    if (wave_ballot(out) != 0) return false;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) yb[lane + 64 * k] = y[k];
+    wave_sync();
+    e.v = yb[0];
+    e.tau = yb[1];
+    e.ton = yb[2];
+    e.b1 = yb[3];
+    e.b2 = yb[4];
+    e.A = yb[5];
+    e.R = yb[6];
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      const int g = RPL * lane + q;
+      e.dr[q] = 7 + g < P ? yb[7 + g] : 0.0;
+    }
+    r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
+    pr = wave_prior_reg<NJ>(y, mu, sg, P, lane);
+    wave_sync();  // yb is rewritten by the next evaluation
+    return true;
+  };
+  RowCursor cur;
+  cur.init(p, s_begin);
+  double u1[NJ], u2[NJ];
+  auto load_u = [&](int64_t s) {
+    const double* src = drow + s * DW;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      const bool in = lane + 64 * k < P;
+      u1[k] = in ? src[lane + 64 * k] : 0.0;
+      u2[k] = in ? src[ld + lane + 64 * k] : 0.0;
+    }
+  };
+  load_u(s_begin);
+  for (int64_t s = s_begin; s <= s_end; ++s) {
+    const double* sc = drow + s * DW + 2 * ld;
+    const double q1 = sc[D_Q1], U1 = sc[D_U1], U2 = sc[D_U2], G = sc[D_G];
+    double y1[NJ], y2[NJ], r1, pr1, r2 = INFINITY, pr2 = 0.0;
+    const bool inb1 = evaluate(u1, 1.0, y1, r1, pr1);
+    // a12 (k_chain lane 0): ssA = r1 (+Inf out of bounds), prA = pr1 (0 out of bounds)
+    const double a12 = fmin(1.0, exp(-0.5 * (r1 - ss) / s2 - 0.5 * (pr1 - prior)));
+    bool acc = false, acc2 = false;
+    if (inb1) {
+      nev += 1;
+      acc = U1 < a12;
+    }
+    if (!acc && p.ntry >= 2) {
+      const bool inb2 = evaluate(u2, inv_ds, y2, r2, pr2);
+      if (inb2) {
+        nev += 1;
+        // a32 (lane 1), l2 (lane 2), a13 (level 3) as k_chain computes them
+        const double a32 = fmin(1.0, exp(-0.5 * (r1 - r2) / s2 - 0.5 * (pr1 - pr2)));
+        const double l2 = exp(-0.5 * (r2 - ss) / s2 - 0.5 * (pr2 - prior));
+        const double a13 = l2 * q1 * (1.0 - a32) / (1.0 - a12);
+        acc2 = U2 < a13;
+      }
+    }
+    if (s < s_end) load_u(s + 1);  // the next row's offsets, while the decision completes
+    if (acc || acc2) {
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) th[k] = acc ? y1[k] : y2[k];
+      ss = acc ? r1 : r2;
+      prior = acc ? pr1 : pr2;
+      nacc += 1;
+    } else {
+      nrej += 1;
+    }
+    // sigma2 Gibbs update of this row (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/ss)
+    if (p.updatesigma) s2 = 1.0 / (G * (2.0 / ss));
+    record_vec_reg<NJ>(st, p, c, s, P, th, smn, sm2, wsv, lane, cur);
+    if (lane == 0) record_s2_cur(st, p, c, s, s2, s2a, cur);
+    cur.next(p);
+  }
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    const int j = lane + 64 * k;
+    if (j < P) {
+      st.theta[c * ld + j] = th[k];
+      st.smean[c * ld + j] = smn[k];
+      st.sm2[c * ld + j] = sm2[k];
+      st.wsumv[c * ld + j] = wsv[k];
+    }
+  }
+  if (lane == 0) {
+    st.ss[c] = ss;
+    st.prior[c] = prior;
+    st.sigma2[c] = s2;
+    st.naccept[c] = nacc;
+    st.nrej_win[c] = nrej;
+    st.nevals[c] = nev;
+    st.s2sum[c] = s2a.sum;
+    st.sq_mean[c] = s2a.qmean;
+    st.sq_m2[c] = s2a.qm2;
+    if (c == 0) *st.step = s_end;  // k_adapt reads the row it follows
+  }
+}
+
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    hipStream_t stream) {
@@ -1157,8 +1325,12 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
   const int64_t per_wg = (int64_t)kDrawSteps * kDrawPasses;
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
   hipLaunchKernelGGL(k_draws, dim3((unsigned)st.n_chains, gy), dim3(kThreads), lds, stream, st, p, s_begin, s_end);
-  hipLaunchKernelGGL((k_chain<RPL, NSEG>), dim3((unsigned)st.n_chains), dim3(kThreads), 0, stream, st, p, kp,
-                     s_begin, s_end);
+  if (p.walk)
+    hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, stream, st, p,
+                       kp, s_begin, s_end);
+  else
+    hipLaunchKernelGGL((k_chain<RPL, NSEG>), dim3((unsigned)st.n_chains), dim3(kThreads), 0, stream, st, p, kp,
+                       s_begin, s_end);
   return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;
 }
 

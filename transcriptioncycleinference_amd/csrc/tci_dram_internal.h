@@ -77,6 +77,7 @@ struct DramParams {
   int64_t lds_matrix;  // bytes of dynamic LDS for the adaptation matrix (0 = work in global memory)
   int64_t pmax;        // max parameter count over the chains (picks the adaptation kernel)
   int64_t chunk;       // fused engine: rows per chain of the draws buffer (>= the longest chunk)
+  int64_t walk;        // fused engine: 1 = one wavefront per chain walks the chunk (k_walk), 0 = k_chain
 };
 
 int dram_launch_init(const DramState& st, const double* qcov_diag, const double* sigma2_0, void* stream);

@@ -53,9 +53,9 @@ class DramOptions:
     stats_from: int = 10000       # chain(n_burn:end, :) (:276)
     thin: int = 0
     seed: int = 20201028
-    engine: str = "auto"          # "auto" | "fused" | "batched" (include/tci.h TCI_DRAM_*): identical chains
+    engine: str = "auto"          # "auto" | "fused" | "batched" | "walk" (include/tci.h TCI_DRAM_*): identical chains
 
-    ENGINES = {"auto": 0, "fused": 1, "batched": 2}
+    ENGINES = {"auto": 0, "fused": 1, "batched": 2, "walk": 3}
 
     def to_c(self, chain_keys: Optional[np.ndarray] = None) -> "_lib.tci_dram_options":
         """``chain_keys`` (int64 [n_chains], kept alive by the caller): chain c's RNG stream key."""
