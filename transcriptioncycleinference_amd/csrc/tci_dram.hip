@@ -820,7 +820,7 @@ struct RowCursor {
 
 // record_vec on register-held vectors by one wave (smn/sm2: this lane's Welford entries): the same
 // stores and Welford arithmetic as record_vec.
-template <int NJ>
+template <int NJ, int SS = 1>  // SS: stride of smn / sm2 / wsv entries (1: registers, 64: a wave's LDS rows)
 __device__ __forceinline__ void record_vec_reg(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P,
                                                const double* th, double* smn, double* sm2, double* wsv,
                                                int lane, const RowCursor& cur) {
@@ -830,7 +830,7 @@ __device__ __forceinline__ void record_vec_reg(const DramState& st, const DramPa
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
       if (lane + 64 * k < P) w[lane + 64 * k] = th[k];
-      wsv[k] = cur.win == 0 ? th[k] : wsv[k] + th[k];  // as record_vec's column sums
+      wsv[SS * k] = cur.win == 0 ? th[k] : wsv[SS * k] + th[k];  // as record_vec's column sums
     }
   }
   if (row >= p.stats_from) {
@@ -839,11 +839,11 @@ __device__ __forceinline__ void record_vec_reg(const DramState& st, const DramPa
     for (int k = 0; k < NJ; ++k) {
       if (lane + 64 * k < P) {
         const double x = th[k];
-        double m = smn[k];
+        double m = smn[SS * k];
         const double d = x - m;
         m += d / n;
-        smn[k] = m;
-        sm2[k] += d * (x - m);
+        smn[SS * k] = m;
+        sm2[SS * k] += d * (x - m);
       }
     }
   }
@@ -1153,7 +1153,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 // one-workgroup-per-chain layout does. Every value is computed by the same expressions as
 // k_chain (its step-s lanes) and the batched engine: identical chains (tests/test_dram_gpu.py).
 #ifndef TCI_WALK_WAVES
-#define TCI_WALK_WAVES 0  // > 0: amdgpu_waves_per_eu register budget for k_walk (A/B)
+#define TCI_WALK_WAVES 2  // amdgpu_waves_per_eu register budget of k_walk (0: none; A/B in DESIGN.md §7)
 #endif
 #if TCI_WALK_WAVES > 0
 #define TCI_WALK_OCC __attribute__((amdgpu_waves_per_eu(TCI_WALK_WAVES)))
@@ -1168,6 +1168,7 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
   constexpr int NW = kThreads / 64;
   __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each wave's {K,J} tables / rows
   __shared__ double yl[NW][64 * NJ];                            // each wave's proposal (theta broadcast)
+  __shared__ double rec[NW][3][64 * NJ];                        // posterior Welford mean / M2, window sums
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * NW + w;
   if (c >= st.n_chains) return;  // uniform per wave; no workgroup barriers below
@@ -1176,7 +1177,10 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
   const int64_t DW = draw_stride(ld);
   const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
   const double inv_ds = 1.0 / p.drscale;
-  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], smn[NJ], sm2[NJ], wsv[NJ];
+  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ];
+  double* smn = &rec[w][0][lane];  // entry k at [64 k] (record_vec_reg<NJ, 64>)
+  double* sm2 = &rec[w][1][lane];
+  double* wsv = &rec[w][2][lane];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
     const int j = lane + 64 * k;
@@ -1186,9 +1190,9 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
     hi[k] = in ? st.upper[c * ld + j] : 0.0;
     mu[k] = in ? st.pmu[c * ld + j] : 0.0;
     sg[k] = in ? st.psig[c * ld + j] : 0.0;
-    smn[k] = in ? st.smean[c * ld + j] : 0.0;
-    sm2[k] = in ? st.sm2[c * ld + j] : 0.0;
-    wsv[k] = in ? st.wsumv[c * ld + j] : 0.0;
+    smn[64 * k] = in ? st.smean[c * ld + j] : 0.0;
+    sm2[64 * k] = in ? st.sm2[c * ld + j] : 0.0;
+    wsv[64 * k] = in ? st.wsumv[c * ld + j] : 0.0;
   }
   EvalIn<RPL> e;  // the chain's cell records stay in registers
   {
@@ -1208,8 +1212,10 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
   int32_t nacc = st.naccept[c], nrej = st.nrej_win[c];
   int64_t nev = st.nevals[c];
   double* yb = yl[w];
-  // ssfun and prior of the proposal th + scale * u (k_chain's per-wave evaluation)
-  auto evaluate = [&](const double* u, double scale, double* y, double& r, double& pr) {
+  // ssfun and prior of the proposal th + scale * u (k_chain's per-wave evaluation); an in-bounds
+  // proposal is left in yb (a move copies it from there)
+  auto evaluate = [&](const double* u, double scale, double& r, double& pr) {
+    double y[NJ];
     bool out = false;
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
@@ -1236,27 +1242,23 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
     }
     r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
     pr = wave_prior_reg<NJ>(y, mu, sg, P, lane);
-    wave_sync();  // yb is rewritten by the next evaluation
     return true;
   };
   RowCursor cur;
   cur.init(p, s_begin);
-  double u1[NJ], u2[NJ];
-  auto load_u = [&](int64_t s) {
-    const double* src = drow + s * DW;
+  // the row's proposal offsets of one stage (loaded when needed: registers, not prefetch, are short)
+  auto load_u = [&](double* u, int64_t s, int stage) {
+    const double* src = drow + s * DW + stage * ld;
 #pragma unroll
-    for (int k = 0; k < NJ; ++k) {
-      const bool in = lane + 64 * k < P;
-      u1[k] = in ? src[lane + 64 * k] : 0.0;
-      u2[k] = in ? src[ld + lane + 64 * k] : 0.0;
-    }
+    for (int k = 0; k < NJ; ++k) u[k] = lane + 64 * k < P ? src[lane + 64 * k] : 0.0;
   };
-  load_u(s_begin);
   for (int64_t s = s_begin; s <= s_end; ++s) {
+    double u[NJ];
+    load_u(u, s, 0);
     const double* sc = drow + s * DW + 2 * ld;
     const double q1 = sc[D_Q1], U1 = sc[D_U1], U2 = sc[D_U2], G = sc[D_G];
-    double y1[NJ], y2[NJ], r1, pr1, r2 = INFINITY, pr2 = 0.0;
-    const bool inb1 = evaluate(u1, 1.0, y1, r1, pr1);
+    double r1, pr1, r2 = INFINITY, pr2 = 0.0;
+    const bool inb1 = evaluate(u, 1.0, r1, pr1);
     // a12 (k_chain lane 0): ssA = r1 (+Inf out of bounds), prA = pr1 (0 out of bounds)
     const double a12 = fmin(1.0, exp(-0.5 * (r1 - ss) / s2 - 0.5 * (pr1 - prior)));
     bool acc = false, acc2 = false;
@@ -1265,7 +1267,8 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
       acc = U1 < a12;
     }
     if (!acc && p.ntry >= 2) {
-      const bool inb2 = evaluate(u2, inv_ds, y2, r2, pr2);
+      load_u(u, s, 1);
+      const bool inb2 = evaluate(u, inv_ds, r2, pr2);
       if (inb2) {
         nev += 1;
         // a32 (lane 1), l2 (lane 2), a13 (level 3) as k_chain computes them
@@ -1275,10 +1278,9 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
         acc2 = U2 < a13;
       }
     }
-    if (s < s_end) load_u(s + 1);  // the next row's offsets, while the decision completes
-    if (acc || acc2) {
+    if (acc || acc2) {  // the accepted proposal is the last one evaluated: it is in yb
 #pragma unroll
-      for (int k = 0; k < NJ; ++k) th[k] = acc ? y1[k] : y2[k];
+      for (int k = 0; k < NJ; ++k) th[k] = yb[lane + 64 * k];
       ss = acc ? r1 : r2;
       prior = acc ? pr1 : pr2;
       nacc += 1;
@@ -1287,7 +1289,8 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
     }
     // sigma2 Gibbs update of this row (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/ss)
     if (p.updatesigma) s2 = 1.0 / (G * (2.0 / ss));
-    record_vec_reg<NJ>(st, p, c, s, P, th, smn, sm2, wsv, lane, cur);
+    wave_sync();  // yb reads are done before the next evaluation rewrites it
+    record_vec_reg<NJ, 64>(st, p, c, s, P, th, smn, sm2, wsv, lane, cur);
     if (lane == 0) record_s2_cur(st, p, c, s, s2, s2a, cur);
     cur.next(p);
   }
@@ -1296,9 +1299,9 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
     const int j = lane + 64 * k;
     if (j < P) {
       st.theta[c * ld + j] = th[k];
-      st.smean[c * ld + j] = smn[k];
-      st.sm2[c * ld + j] = sm2[k];
-      st.wsumv[c * ld + j] = wsv[k];
+      st.smean[c * ld + j] = smn[64 * k];
+      st.sm2[c * ld + j] = sm2[64 * k];
+      st.wsumv[c * ld + j] = wsv[64 * k];
     }
   }
   if (lane == 0) {
