@@ -229,11 +229,12 @@ __device__ __forceinline__ void store_R(const DramState& st, int64_t c, int P, i
   st.R[c * st.ld * st.ld + (int64_t)i * st.ld + j] = v;
   if (j >= i) st.Rf[c * tri_stride(st.ld) + tri_off(i, P) + j - i] = (float)v;
 }
+template <int NTH = kThreads>
 __device__ void load_R_f32(float* Rl, const DramState& st, int64_t c, int P) {
   const float* src = st.Rf + c * tri_stride(st.ld);
   const int tri = P * (P + 1) / 2;
 #pragma unroll 4
-  for (int e = threadIdx.x; e < tri; e += kThreads) Rl[e] = src[e];
+  for (int e = threadIdx.x; e < tri; e += NTH) Rl[e] = src[e];
 }
 
 // Proposal products U[r][j] = sum_{i<=j} Z[r][i] R[i][j] for r < M <= 16*MT rows of normals (LDS,
@@ -248,7 +249,7 @@ __device__ void load_R_f32(float* Rl, const DramState& st, int64_t c, int P) {
 // instance (the batched engine's 1-row proposals, the fused engine's 32-row draws) gives the same
 // bits.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-template <int MT, int CT, class Store>
+template <int MT, int CT, int NWV, class Store>  // NWV: waves sharing the column tiles
 __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const float* Rl, int P, Store store) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int row = lane & 15, kq = lane >> 4;
@@ -256,7 +257,7 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
   int nt[CT], kmx[CT];
 #pragma unroll
   for (int g = 0; g < CT; ++g) {
-    nt[g] = ntiles - 1 - (4 * g + ((g & 1) ? 3 - w : w));  // uniform: costliest tiles first, snake order
+    nt[g] = ntiles - 1 - (NWV * g + ((g & 1) ? NWV - 1 - w : w));  // uniform: costliest first, snake order
     kmx[g] = nt[g] >= 0 ? min(16 * nt[g] + 15, P - 1) : -1;
   }
   // The tiles are in decreasing k-extent (kmx[0] >= kmx[1] >= ..), so the k-steps split into
@@ -361,7 +362,7 @@ __device__ bool propose_block(const DramState& st, const DramParams& p, int64_t 
   __syncthreads();
   double* U = sm.y;
   const int us = sm.L;
-  mfma_zr<1, kZrCT>(sm.z, sm.L, 1, sm.Rl, P, [=](int r, int j, double v) { U[r * us + j] = v; });
+  mfma_zr<1, kZrCT, 4>(sm.z, sm.L, 1, sm.Rl, P, [=](int r, int j, double v) { U[r * us + j] = v; });
   __syncthreads();
   int inb = 1;
   for (int j = threadIdx.x; j < P; j += kThreads) {
@@ -704,11 +705,12 @@ __global__ __launch_bounds__(kThreads) void k_adapt(DramState st, DramParams p) 
 
 // Normals of both stages for `ns` steps from `step` into rows 2 k (stage 1, P_NORM1) and 2 k + 1
 // (stage 2, P_NORM2) of Z (row stride L), one Philox call per thread and round.
+template <int NTH>
 __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int64_t step, int ns, int P, bool two,
                                                    double* Z, int L) {
   const int np = (P + kNPer - 1) / kNPer;
   const int rows = 2 * ns;
-  for (int k = threadIdx.x; k < rows * np; k += kThreads) {
+  for (int k = threadIdx.x; k < rows * np; k += NTH) {
     const int r = k / np, q = k - r * np;
     double* z = Z + r * L;
     double n[kNPer];
@@ -741,7 +743,13 @@ __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
   return (2 * kDrawSteps * L) * 8 + (L * (L + 1) / 2) * 4 + 16;
 }
 
-__global__ __launch_bounds__(kThreads) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end) {
+// NWD waves per workgroup: 4 for the FUSED engine (299 TestData chains: 100.6 vs 105.4 ms per 20k
+// steps with 8), 8 for WALK (10,000 chains, one workgroup per CU at P = 207: 175 vs 188 ms per
+// 1000 steps with 4). The wave count only moves column tiles between waves: same bits.
+template <int NWD>
+__global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end) {
+  constexpr int kDrawWaves = NWD, kDrawThreads = 64 * NWD;
+  constexpr int kDrawCT = (kZrCT * 4 + kDrawWaves - 1) / kDrawWaves;  // column tiles per wave (P <= 320)
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
@@ -753,7 +761,7 @@ __global__ __launch_bounds__(kThreads) void k_draws(DramState st, DramParams p, 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   double* Z = dyn;
   float* Rl = reinterpret_cast<float*>(Z + 2 * kDrawSteps * L);
-  if (!(TCI_DRAWS_ABLATE & 8)) load_R_f32(Rl, st, c, P);
+  if (!(TCI_DRAWS_ABLATE & 8)) load_R_f32<kDrawThreads>(Rl, st, c, P);
   const double a = 0.5 * (double)st.nobs[c];
   const double inv_ds = 1.0 / p.drscale;
   double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
@@ -761,14 +769,14 @@ __global__ __launch_bounds__(kThreads) void k_draws(DramState st, DramParams p, 
     const int64_t step0 = s_begin + ((int64_t)blockIdx.y * kDrawPasses + pass) * kDrawSteps;
     if (step0 > s_end) break;  // uniform over the workgroup
     const int ns = (int)min<int64_t>(kDrawSteps, s_end - step0 + 1);
-    if (!(TCI_DRAWS_ABLATE & 1)) draw_block_normals(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
+    if (!(TCI_DRAWS_ABLATE & 1)) draw_block_normals<kDrawThreads>(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
     __syncthreads();  // (the first pass: also R)
     // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
     double* d0 = drow + step0 * DW;
     if (!(TCI_DRAWS_ABLATE & 2))
-      mfma_zr<kDrawMT, kZrCT>(Z, L, 2 * ns, Rl, P,
+      mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rl, P,
                               [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; });
-    for (int k = w; k < ns; k += kThreads / 64) {
+    for (int k = w; k < ns; k += kDrawWaves) {
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
       if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
     }
@@ -1322,12 +1330,13 @@ template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    hipStream_t stream) {
   const size_t lds = (size_t)draws_lds_bytes(st.ld);
+  auto kd = p.walk ? k_draws<8> : k_draws<4>;
   if (lds > 48 * 1024 &&
-      hipFuncSetAttribute((const void*)k_draws, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return TCI_EHIP;
   const int64_t per_wg = (int64_t)kDrawSteps * kDrawPasses;
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
-  hipLaunchKernelGGL(k_draws, dim3((unsigned)st.n_chains, gy), dim3(kThreads), lds, stream, st, p, s_begin, s_end);
+  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(p.walk ? 512 : 256), lds, stream, st, p, s_begin, s_end);
   if (p.walk)
     hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, stream, st, p,
                        kp, s_begin, s_end);
