@@ -13,7 +13,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_IN
   i=$((i+1))
   echo "== pass $i: $grp"
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/${TAG}_p$i" -o pmc -- \
-    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --dram-steps 0 > "$OUT/${TAG}_p$i.json" 2> "$OUT/${TAG}_p$i.err"
+    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --dram-steps 0 --no-configs > "$OUT/${TAG}_p$i.json" 2> "$OUT/${TAG}_p$i.err"
   rc=$?
   if [ $rc -ne 0 ]; then echo "pass $i status $rc"; tail -5 "$OUT/${TAG}_p$i.err"; exit $rc; fi
 done
