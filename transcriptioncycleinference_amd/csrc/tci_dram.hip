@@ -1185,6 +1185,10 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
   const int64_t DW = draw_stride(ld);
   const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
   const double inv_ds = 1.0 / p.drscale;
+  // Bounds and prior vectors: held in registers for one segment per dye; re-read from global
+  // memory at every evaluation for NSEG >= 2, whose larger evaluation spilled 108 B per lane at
+  // the 2-waves/SIMD budget (config 5: 230 -> 206 ms per 1000 steps; config 4 unchanged).
+  constexpr bool kGB = NSEG >= 2;
   double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ];
   double* smn = &rec[w][0][lane];  // entry k at [64 k] (record_vec_reg<NJ, 64>)
   double* sm2 = &rec[w][1][lane];
@@ -1194,10 +1198,12 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
     const int j = lane + 64 * k;
     const bool in = j < P;
     th[k] = in ? st.theta[c * ld + j] : 0.0;
-    lo[k] = in ? st.lower[c * ld + j] : 0.0;
-    hi[k] = in ? st.upper[c * ld + j] : 0.0;
-    mu[k] = in ? st.pmu[c * ld + j] : 0.0;
-    sg[k] = in ? st.psig[c * ld + j] : 0.0;
+    if (!kGB) {
+      lo[k] = in ? st.lower[c * ld + j] : 0.0;
+      hi[k] = in ? st.upper[c * ld + j] : 0.0;
+      mu[k] = in ? st.pmu[c * ld + j] : 0.0;
+      sg[k] = in ? st.psig[c * ld + j] : 0.0;
+    }
     smn[64 * k] = in ? st.smean[c * ld + j] : 0.0;
     sm2[64 * k] = in ? st.sm2[c * ld + j] : 0.0;
     wsv[64 * k] = in ? st.wsumv[c * ld + j] : 0.0;
@@ -1225,6 +1231,17 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
   auto evaluate = [&](const double* u, double scale, double& r, double& pr) {
     double y[NJ];
     bool out = false;
+    if constexpr (kGB) {
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) {
+        const int j = lane + 64 * k;
+        const bool in = j < P;
+        lo[k] = in ? st.lower[c * ld + j] : 0.0;
+        hi[k] = in ? st.upper[c * ld + j] : 0.0;
+        mu[k] = in ? st.pmu[c * ld + j] : 0.0;
+        sg[k] = in ? st.psig[c * ld + j] : 0.0;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
       y[k] = th[k] + scale * u[k];
