@@ -17,6 +17,7 @@ OUT = os.path.join(ROOT, "build", "ab")
 VARIANTS = {
     "ship": [],
     "old": None,  # a prebuilt library of the previous commit, copied to build/ab/libtci_old.so
+    "adapt16": ["TCI_ADAPT_WAVES13=16"],
     "abl_rows": ["TCI_ABLATE=1"],
     "abl_bounds": ["TCI_ABLATE=2"],
     "abl_interp": ["TCI_ABLATE=4"],

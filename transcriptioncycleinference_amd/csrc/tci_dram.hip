@@ -1682,19 +1682,19 @@ __device__ __forceinline__ void chol16_finish(double (&a)[4], int lane, double* 
 // per wave (MAXT (MAXT + 1) / 2 <= NW kAdOwn): <4, 9> for P <= 144 (two chains per CU), <8, 13>
 // for P <= 208 (configs 4/5: 200 points, P = 207; one chain per CU at 256 VGPRs per wave).
 constexpr int kAdRB = 16;   // window rows per LDS batch
-constexpr int kAdOwn = 12;  // output tiles per wave (a multiple of the merge group kAdMG)
 __host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P) {
   const int64_t NT = (P + 15) / 16, LX = 16 * NT;
   const int64_t shared = kAdRB * LX > 2 * NT * 256 ? kAdRB * LX : 2 * NT * 256;  // X | panel buffers
   return (shared + 2 * LX) * 8;
 }
 
-template <int NW, int MAXT>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_adapt_mfma(DramState st,
-                                                                                              DramParams p) {
+template <int NW, int MAXT, int kAdOwn>  // kAdOwn: output tiles per wave (a multiple of the merge group)
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8 ? 2 : NW / 4))) void k_adapt_mfma(
+    DramState st, DramParams p) {
   constexpr int kAdM = MAXT;
   constexpr int NTH = 64 * NW;
   static_assert(MAXT * (MAXT + 1) / 2 <= NW * kAdOwn, "owned tiles per wave");
+  static_assert(kAdOwn % 6 == 0, "owned tiles come in merge groups of 6");
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int fail;
   __shared__ double rdg[16];  // 1 / U[k][k] of the current diagonal tile
@@ -1957,10 +1957,10 @@ int launch_stage(void (*k)(DramState, DramParams), const DramState& st, const Dr
   return finish();
 }
 
-template <int NW, int MAXT>
+template <int NW, int MAXT, int OWN>
 int launch_adapt_mfma(const DramState& st, const DramParams& p, void* stream) {
   const size_t bytes = (size_t)adapt_mfma_lds_bytes(p.pmax);
-  auto k = k_adapt_mfma<NW, MAXT>;
+  auto k = k_adapt_mfma<NW, MAXT, OWN>;
   if (bytes > 48 * 1024 &&
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
     return TCI_EHIP;
@@ -1991,8 +1991,15 @@ int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream) 
   return launch_stage(k_accept2, st, p, stream);
 }
 int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
-  if (p.pmax <= 16 * 9) return launch_adapt_mfma<4, 9>(st, p, stream);
-  if (p.pmax <= 16 * 13) return launch_adapt_mfma<8, 13>(st, p, stream);
+  if (p.pmax <= 16 * 9) return launch_adapt_mfma<4, 9, 12>(st, p, stream);
+#ifndef TCI_ADAPT_WAVES13
+#define TCI_ADAPT_WAVES13 8  // waves per chain of the P <= 208 adaptation (16 waves x 6 tiles: A/B, slower)
+#endif
+#if TCI_ADAPT_WAVES13 == 16
+  if (p.pmax <= 16 * 13) return launch_adapt_mfma<16, 13, 6>(st, p, stream);
+#else
+  if (p.pmax <= 16 * 13) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
+#endif
   const int64_t ntile = (p.pmax + 3) / 4;
   if (ntile * (ntile + 1) / 2 <= (int64_t)kAdaptTiles * kThreads && adapt_tiles_lds_bytes(p.pmax) <= 78 * 1024) {
     const size_t bytes = (size_t)adapt_tiles_lds_bytes(p.pmax);
