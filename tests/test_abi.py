@@ -92,3 +92,14 @@ def test_create_rejects_bad_input_before_touching_a_device(lib):
     assert rc == _lib.TCI_EINVAL
     rc, msg = create(np.arange(600.0), [0, 600])
     assert rc == _lib.TCI_EINVAL and "max" in msg
+
+
+def test_dram_engine_codes_match_the_header():
+    """DramOptions.ENGINES (Python) carries the same codes as include/tci.h's TCI_DRAM_*."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions
+
+    src = open(os.path.join(ROOT, "include", "tci.h")).read()
+    hdr = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"#define TCI_DRAM_([A-Z]+) (\d+)", src)}
+    assert hdr == DramOptions.ENGINES
+    with pytest.raises(ValueError):
+        DramOptions(engine="lockstep").to_c()
