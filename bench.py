@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Benchmark: forward-model SS evaluations/sec on the 299-cell TestData (BASELINE.json metric).
 
-One *step* = one batched ssfun launch over the whole per-GPU workload: every TestData cell
-(299) x P DRAM-style proposals (default 256), i.e. the evaluations mcmcstat would request
-from 299 independent chains over P lockstep proposals. Proposals are Gaussian around the
+One *launch* = one batched ssfun evaluation of the whole per-GPU workload: every TestData cell
+(299) x K DRAM-style proposals (default 256), i.e. the evaluations mcmcstat would request from
+299 independent chains over K lockstep proposals. One *step* = --launches-per-step (128) such
+launches over distinct resident proposal batches, so the timed region is >= 100 ms at the default
+--steps 20. Proposals are Gaussian around the
 fixture chain states with the reference's proposal variances J0 (TranscriptionCycleMCMC.m:
 217-231); proposals outside the parameter box (:242-255) are marked inactive and are NOT
 counted (mcmcstat rejects them without calling ssfun). All inputs are resident in HBM before
@@ -13,6 +15,10 @@ Multi-GPU (torchrun, one process per GPU, RCCL): weak scaling -- every rank eval
 replica of the 299-cell workload with a rank-specific seed; there is no data-path collective.
 The per-cell results are gathered once after timing (the reference's parfor output assembly),
 and the elapsed time is the max over ranks.
+
+Beside `value` (kernel mode, K = 256) the line carries the K in {1, 64, 256, 1024} sweep, the
+drop-in's per-call latency, the metric's 200k-step end-to-end fit (BASELINE config 2), configs
+3/4/5, and the CPU baseline at all host threads and at one core.
 
 Prints ONE JSON line on rank 0.
 """
@@ -36,7 +42,7 @@ CONSTRUCT = "P2P-MS2v5-LacZ-PP7v4"
 
 
 def proposal_batch(cells, P: int, seed: int):
-    """theta (B, ld), cell_id (B,), active (B,) for 299 cells x P proposals."""
+    """theta (B, ld), cell_id (B,), active (B,) for 299 cells x P proposals (host, numpy)."""
     from transcriptioncycleinference_amd.data import DR_BOUNDS, LOWER, UPPER
 
     with np.load(os.path.join(ROOT, "tests", "golden", "chain_theta.npz"), allow_pickle=False) as f:
@@ -66,6 +72,60 @@ def proposal_batch(cells, P: int, seed: int):
         dR = theta[c * P:(c + 1) * P, 7:7 + n]
         active[c * P:(c + 1) * P] &= np.all((dR >= DR_BOUNDS[0]) & (dR <= DR_BOUNDS[1]), axis=1)
     return theta, cid, active.astype(np.uint8)
+
+
+class ProposalRounds:
+    """``rounds`` distinct lockstep proposal batches for 299 cells x K proposals, generated and kept
+    resident in HBM (one batch = what 299 DRAM chains would hand ssfun at one step if each proposed
+    K candidates): theta = a fixture chain state of the cell + N(0, J0) (the reference's proposal
+    variances, TranscriptionCycleMCMC.m:217-231); rows outside the parameter box (:242-255) are
+    inactive and not counted (mcmcstat rejects them without calling ssfun). Cycling through distinct
+    batches keeps every launch's theta reads coming from memory, not from a cache warmed by the
+    previous launch of the same batch."""
+
+    def __init__(self, cells, K: int, rounds: int, seed: int, dev):
+        import torch
+
+        from transcriptioncycleinference_amd.data import DR_BOUNDS, LOWER, UPPER
+
+        with np.load(os.path.join(ROOT, "tests", "golden", "chain_theta.npz"), allow_pickle=False) as f:
+            z = {k: f[k] for k in f.files}
+        C, lens = cells.n_cells, cells.lengths.astype(np.int64)
+        ld = int(7 + lens.max())
+        off = z["theta_offsets"]
+        S = np.zeros((len(off) - 1, ld))
+        for i in range(len(off) - 1):
+            S[i, :off[i + 1] - off[i]] = z["theta"][off[i]:off[i + 1]]
+        first = np.searchsorted(z["cell_id"], np.arange(C))            # rows are sorted by cell
+        count = np.bincount(z["cell_id"], minlength=C)
+        sd = np.zeros((C, ld))
+        lo, hi = np.zeros((C, ld)), np.zeros((C, ld))
+        for c in range(C):
+            n = int(lens[c])
+            t = cells.cell(c)[0]
+            sd[c, :7 + n] = np.sqrt(np.concatenate([[0.05, 0.1, t[-1] - t[-2], 1.0, 1.0, 0.05, 0.5], np.full(n, 0.5)]))
+            lo[c, :7], hi[c, :7] = LOWER, UPPER
+            lo[c, 7:], hi[c, 7:] = DR_BOUNDS
+        self.B, self.ld, self.K = C * K, ld, K
+        cid = np.repeat(np.arange(C, dtype=np.int32), K)
+        g = torch.Generator(device=dev)
+        g.manual_seed(int(seed))
+        S_d, sd_d = torch.from_numpy(S).to(dev), torch.from_numpy(sd).to(dev)
+        lo_d, hi_d = torch.from_numpy(lo).to(dev), torch.from_numpy(hi).to(dev)
+        cid_l = torch.from_numpy(cid.astype(np.int64)).to(dev)
+        first_d, count_d = torch.from_numpy(first).to(dev), torch.from_numpy(count).to(dev)
+        self.cid = torch.from_numpy(cid).to(dev)
+        self.theta, self.active, self.n_active = [], [], []
+        for _ in range(rounds):
+            u = torch.rand(self.B, generator=g, device=dev, dtype=torch.float64)
+            pick = first_d[cid_l] + torch.clamp((u * count_d[cid_l]).long(), max=int(count.max()) - 1)
+            th = S_d[pick] + torch.randn(self.B, ld, generator=g, device=dev, dtype=torch.float64) * sd_d[cid_l]
+            act = ((th >= lo_d[cid_l]) & (th <= hi_d[cid_l])).all(dim=1).to(torch.uint8)
+            self.theta.append(th.contiguous())
+            self.active.append(act)
+            self.n_active.append(int(act.sum().item()))
+        self.cid_host = cid
+        self.out = torch.empty(self.B, dtype=torch.float64, device=dev)
 
 
 def algorithmic_bytes(cells, cid, active) -> int:
@@ -105,33 +165,44 @@ def valu_issue(pmc: dict, kernel_ms: float):
             "valu_insts_per_launch": insts, "source": pmc.get("source")}
 
 
-def cpu_baseline(cells, theta, cid, active, seconds: float):
-    """The C oracle (faithful matrix-form restatement, OpenMP over rows -- the parfor analogue)
-    on the host cores, on a bounded sample of the same workload."""
-    from oracle import c_oracle, oracle as ref  # cpu_baseline leg only
+def _cpu_rate(cells, cs, th, ci, ac, threads: int, seconds: float):
+    from oracle import c_oracle  # cpu_baseline leg only
 
-    c_oracle.build()
-    cs = ref.builtin_construct(CONSTRUCT)
-    threads = c_oracle.max_threads()
-    # sample: every cell, the first proposals of each, enough rows to keep all threads busy
-    P = len(cid) // cells.n_cells
-    per_cell = max(1, min(P, (threads * 8 + cells.n_cells - 1) // cells.n_cells))
-    idx = np.concatenate([np.arange(c * P, c * P + per_cell) for c in range(cells.n_cells)])
-    th, ci, ac = theta[idx], cid[idx], active[idx]
     n_act = int(ac.sum())
-    evals, t0 = 0, time.perf_counter()
-    reps = 0
+    evals, reps, t0 = 0, 0, time.perf_counter()
     while True:
         c_oracle.ss_batch(cells.offsets, cells.t, cells.ms2, cells.pp7, cs, th, ci, ac, nthreads=threads)
         evals += n_act
         reps += 1
         el = time.perf_counter() - t0
         if el >= seconds:
-            break
-    return {"value": evals / el, "unit": "SS evals/s", "cores": threads, "kind": "port",
-            "sample": f"{len(idx)} rows ({per_cell} proposals x {cells.n_cells} cells, {n_act} in-bounds) x {reps} "
-                      f"passes = {evals} evals in {el:.1f} s; C matrix-form oracle (oracle/tci_oracle.c), "
-                      f"OpenMP {threads} threads"}
+            return evals / el, evals, reps, el
+
+
+def cpu_baseline(cells, theta, cid, active, seconds: float):
+    """The C oracle (faithful matrix-form restatement, OpenMP over rows -- the parfor analogue)
+    on the host cores, on a bounded sample of the same workload: every cell, its first proposals,
+    enough rows to keep every thread busy. Reported at all host threads (the box's CPU share:
+    OMP_NUM_THREADS) and at 1 core (BASELINE.md's CPU-baseline plan)."""
+    from oracle import c_oracle, oracle as ref  # cpu_baseline leg only
+
+    c_oracle.build()
+    cs = ref.builtin_construct(CONSTRUCT)
+    threads = c_oracle.max_threads()
+    P = len(cid) // cells.n_cells
+    per_cell = max(1, min(P, (threads * 8 + cells.n_cells - 1) // cells.n_cells))
+    idx = np.concatenate([np.arange(c * P, c * P + per_cell) for c in range(cells.n_cells)])
+    th, ci, ac = theta[idx], cid[idx], active[idx]
+    rate, evals, reps, el = _cpu_rate(cells, cs, th, ci, ac, threads, seconds)
+    one = np.arange(cells.n_cells) * per_cell          # one proposal per cell for the 1-core leg
+    rate1, evals1, reps1, el1 = _cpu_rate(cells, cs, th[one], ci[one], ac[one], 1, seconds / 2)
+    return {"value": rate, "unit": "SS evals/s", "cores": threads, "kind": "port",
+            "sample": f"{len(idx)} rows ({per_cell} proposals x {cells.n_cells} cells, {int(ac.sum())} in-bounds) x "
+                      f"{reps} passes = {evals} evals in {el:.1f} s; C matrix-form oracle (oracle/tci_oracle.c), "
+                      f"OpenMP {threads} threads",
+            "single_core": {"value": rate1, "unit": "SS evals/s", "cores": 1,
+                            "sample": f"{len(one)} rows (1 proposal x {cells.n_cells} cells) x {reps1} passes = "
+                                      f"{evals1} evals in {el1:.1f} s"}}
 
 
 def end_to_end(lk, n_steps: int, seed: int, reduce=None):
@@ -235,8 +306,7 @@ def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_s
     """SURVEY.md §8(d) configs 4/5 end to end: this rank's shard of the 10,000 synthetic cells
     fitted by the GPU-resident DRAM (one chain per cell, n_burn = n_steps/20), as
     `parallel.fit_sharded` runs it minus the results gather. Strong scaling: 10,000 cells in total.
-    n_steps is a bounded sample of the reference's 200k (the per-step cost is constant once the
-    first adaptation has run; stated in the output)."""
+    BASELINE configs 4/5 name n_steps = 200000 (the default); a smaller n_steps is labelled a sample."""
     from transcriptioncycleinference_amd import Likelihood
     from transcriptioncycleinference_amd.mcmc import DramOptions, fit
 
@@ -248,7 +318,8 @@ def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_s
         wall = reduce(time.perf_counter() - t0, "max")
     dev_s, evals = reduce(fr.elapsed_ms * 1e-3, "max"), int(reduce(fr.n_evals, "sum"))
     return {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points, construct {construct.name}, "
-                        f"{hi - lo} chains on rank 0, {n_steps} steps (bounded sample of 200k)",
+                        f"{hi - lo} chains on rank 0, {n_steps} steps"
+                        + ("" if n_steps >= 200000 else " (bounded sample of the configured 200k)"),
             "n_steps": n_steps, "engine": engine, "chains": int(reduce(len(fr.MCMCresults), "sum")), "device_s": dev_s,
             "wall_s": wall, "ssfun_evals": evals, "value": evals / dev_s, "unit": "SS evals/s", "scaling": "strong",
             "us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
@@ -275,20 +346,102 @@ def hierarchical_end_to_end(lk, n_steps: int, seed: int, reduce):
                                 for r in fr.MCMCresults))}
 
 
+def kernel_mode(lk, rounds: ProposalRounds, launches: int, stream, sync_ranks=None):
+    """``launches`` back-to-back batched launches cycling over the resident proposal rounds, timed
+    with HIP events on the launch stream (per-launch kernel time) and the wall clock (whole job).
+    Returns (wall seconds, kernel ms per launch, in-bounds evals)."""
+    import torch
+
+    R = len(rounds.theta)
+    torch.cuda.synchronize()
+    if sync_ranks:
+        sync_ranks()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for i in range(launches):
+        r = i % R
+        lk.ss_batch_device(rounds.theta[r], rounds.cid, rounds.out, rounds.active[r], stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if sync_ranks:
+        sync_ranks()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    evals = sum(rounds.n_active[i % R] for i in range(launches))
+    return wall, e0.elapsed_time(e1) / launches, evals
+
+
+def rounds_algorithmic_bytes(cells, rounds: ProposalRounds) -> float:
+    """Mean algorithmic bytes per launch over the rounds (see algorithmic_bytes)."""
+    return float(np.mean([algorithmic_bytes(cells, rounds.cid_host, a.cpu().numpy()) for a in rounds.active]))
+
+
+def kernel_sweep(lk, cells, dev, stream, seed: int, Ks=(1, 64, 256, 1024), target_s: float = 0.05):
+    """kernel throughput at K proposals per cell per launch (B = 299 K rows).
+    K = 1 is the reference's own per-step batch (one ssfun per parfor cell)."""
+    out = []
+    for K in Ks:
+        rounds = ProposalRounds(cells, K, 4, seed + K, dev)
+        kernel_mode(lk, rounds, 4, stream)                                  # warm-up
+        _, ms, _ = kernel_mode(lk, rounds, 8, stream)
+        n = int(max(16, min(20000, target_s / max(ms * 1e-3, 1e-7))))
+        wall, ms, evals = kernel_mode(lk, rounds, n, stream)
+        alg = rounds_algorithmic_bytes(cells, rounds)
+        ach = alg / (ms * 1e-3) / 1e9
+        out.append({"K": K, "rows_per_launch": rounds.B, "in_bounds_per_launch": float(np.mean(rounds.n_active)),
+                    "launches": n, "kernel_us": ms * 1e3, "value": evals / wall, "unit": "SS evals/s",
+                    "kernel_evals_per_s": float(np.mean(rounds.n_active)) / (ms * 1e-3),
+                    "algorithmic_bytes_per_launch": alg, "achieved_GBs": ach, "hbm_frac": ach / HBM_PEAK_GBS})
+        del rounds
+    return out
+
+
+def drop_in_latency(lk, cells, theta, cid, calls: int = 2000):
+    """Per-call latency of the literal drop-in: ``tci_ssfun`` (one ssfun(theta, data) with its H2D
+    copy, launch, D2H copy and synchronisation -- what mcmcstat's DRAM loop calls once or twice per
+    step, TranscriptionCycleMCMC.m:186,258), and ``tci_ss_batch`` on host pointers with one row per
+    cell (the lockstep driver's per-step call for all 299 chains, K = 1)."""
+    rows = [np.ascontiguousarray(theta[np.nonzero(cid == c)[0][0], :7 + int(cells.lengths[c])]) for c in range(8)]
+    for k in range(50):
+        lk.ssfun(rows[k % 8], k % 8)
+    t0 = time.perf_counter()
+    for k in range(calls):
+        lk.ssfun(rows[k % 8], k % 8)
+    one = (time.perf_counter() - t0) / calls
+    first = np.array([np.nonzero(cid == c)[0][0] for c in range(cells.n_cells)])
+    th, ci = np.ascontiguousarray(theta[first]), np.ascontiguousarray(cid[first])
+    for _ in range(20):
+        lk.ss_batch(th, ci)
+    n_b = max(200, calls // 4)
+    t0 = time.perf_counter()
+    for _ in range(n_b):
+        lk.ss_batch(th, ci)
+    batch = (time.perf_counter() - t0) / n_b
+    return {"tci_ssfun_us_per_call": one * 1e6, "tci_ssfun_calls_per_s": 1.0 / one,
+            "ss_batch_299_rows_us_per_call": batch * 1e6, "ss_batch_299_rows_evals_per_s": cells.n_cells / batch,
+            "note": "host pointers, synchronous, PCIe round trip included; Python ctypes call overhead included"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--proposals", type=int, default=256, help="DRAM-style proposals per cell per launch")
+    ap.add_argument("--proposals", type=int, default=256, help="DRAM-style proposals per cell per launch (K)")
+    ap.add_argument("--launches-per-step", type=int, default=128,
+                    help="batched launches per step: one step = this many lockstep proposal rounds")
+    ap.add_argument("--distinct-rounds", type=int, default=8, help="distinct resident proposal batches cycled")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the K in {1, 64, 256, 1024} kernel sweep")
     ap.add_argument("--dram-steps", type=int, default=200000,
                     help="end-to-end mode: one DRAM chain per TestData cell for this many steps (0 = skip)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the other BASELINE configs (3: hierarchical fit; 4/5: 10k synthetic cells)")
-    ap.add_argument("--synth-dram-steps", type=int, default=2000,
-                    help="configs 4/5 end to end: DRAM steps of the 10,000-chain fit (a bounded sample of 200k; 0 = skip)")
+    ap.add_argument("--synth-dram-steps", type=int, default=200000,
+                    help="configs 4/5 end to end: DRAM steps of the 10,000-chain fit (BASELINE: 200k; 0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -310,70 +463,48 @@ def main():
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
     dev = torch.device("cuda", device_index)
+    torch.cuda.set_device(dev)
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
+
+    def reduce(x, op):
+        if not distributed:
+            return x
+        t = torch.tensor([float(x)], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        return float(t.item())
+
+    barrier = dist.barrier if distributed else None
 
     from transcriptioncycleinference_amd import Likelihood, testdata
 
     cells = testdata()
-    theta, cid, active = proposal_batch(cells, args.proposals, seed=20201028 + rank)
-    B, ld = theta.shape
-    n_active = int(active.sum())
     lk = Likelihood(cells, CONSTRUCT, device=device_index)
-    th_d = torch.from_numpy(theta).to(dev)
-    cid_d = torch.from_numpy(cid).to(dev)
-    act_d = torch.from_numpy(active).to(dev)
-    out_d = torch.empty(B, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
-
-    def step():
-        lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
+    rounds = ProposalRounds(cells, args.proposals, args.distinct_rounds, 20201028 + rank, dev)
+    L = args.launches_per_step
+    kernel_mode(lk, rounds, max(1, args.warmup) * L, stream)                         # untimed warm-up steps
+    wall, kernel_ms, evals = kernel_mode(lk, rounds, args.steps * L, stream, sync_ranks=barrier)
+    elapsed = reduce(wall, "max")
+    total_active = int(reduce(evals, "sum"))
+    ss = rounds.out.cpu().numpy()
+    act_last = rounds.active[(args.steps * L - 1) % len(rounds.theta)].cpu().numpy().astype(bool)
+    finite_ok = bool(np.all(np.isfinite(ss[act_last])))
     if distributed:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(args.steps):
-        step()
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    kernel_ms = e0.elapsed_time(e1) / args.steps  # per launch, HIP events on the launch stream
-
-    ss = out_d.cpu().numpy()
-    finite_ok = bool(np.all(np.isfinite(ss[active.astype(bool)])))
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        cnt = torch.tensor([n_active], dtype=torch.int64, device=coll_dev)
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-        total_active = int(cnt.item())
         # the one results collective: per-cell SS of the last proposal of every cell (RCCL)
         from transcriptioncycleinference_amd.parallel import gather_rows
 
         per_cell = ss.reshape(cells.n_cells, -1)[:, -1].copy()
         gathered = gather_rows(per_cell, device=str(coll_dev))
         assert len(gathered) == cells.n_cells * world
-    else:
-        total_active = n_active
 
     workload = f"TestData-299cells-x{args.proposals}proposals"
-    alg = algorithmic_bytes(cells, cid, active)
+    alg = rounds_algorithmic_bytes(cells, rounds)
     achieved = alg / (kernel_ms * 1e-3) / 1e9
     pmc = load_pmc(workload)
     traffic = pmc.get("hbm_bytes_per_launch")
     res = {
         "metric": "forward-model SS evals/sec, 299-cell TestData, 200k-step chains @1/2/4/8 GPU",
-        "value": total_active * args.steps / elapsed,
+        "value": total_active / elapsed,
         "unit": "SS evals/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -386,10 +517,14 @@ def main():
         "data": "reference TestData.mat (299 cells) + synthetic DRAM-style proposals around the fixture chain states",
         "config": {
             "workload": workload,
+            "step": f"{L} batched launches, each one lockstep round of {args.proposals} proposals for each of the "
+                    f"{cells.n_cells} cells ({args.distinct_rounds} distinct resident proposal batches cycled)",
             "cells_per_gpu": cells.n_cells,
             "proposals_per_cell": args.proposals,
-            "rows_per_step_per_gpu": B,
-            "in_bounds_evals_per_step_per_gpu": n_active,
+            "launches_per_step": L,
+            "rows_per_launch_per_gpu": rounds.B,
+            "in_bounds_evals_per_launch_per_gpu": float(np.mean(rounds.n_active)),
+            "timed_region_s": elapsed,
             "construct": CONSTRUCT,
             "parallelism": f"replica-per-gpu x{world} (cells independent; 1 RCCL gather after timing)",
             "kernel_rows_per_lane": lk.info["rows_per_lane"],
@@ -403,57 +538,56 @@ def main():
             "traffic": traffic,
             "kernel_ms": kernel_ms,
             "algorithmic_bytes_per_launch": alg,
-            "note": "FP64-VALU-issue-bound path (see 'valu'); HBM fraction reported as the north star asks (DESIGN.md §3)",
+            "note": "VALU-issue/latency-bound FP64 path (see 'valu'); HBM fraction reported as the north star asks "
+                    "(DESIGN.md §3)",
             "valu": valu_issue(pmc, kernel_ms),
         },
         "results_finite": finite_ok,
     }
+    if not args.no_sweep:
+        res["kernel_sweep"] = kernel_sweep(lk, cells, dev, stream, seed=77 + rank)
+    theta_h = rounds.theta[0].cpu().numpy()
+    act_h = rounds.active[0].cpu().numpy()
     if rank == 0 and world == 1:
-        # PCIe-inclusive rate of the host-pointer entry point (theta H2D + SS D2H per call):
-        # reported beside, never as, `value`.
-        lk.ss_batch(theta, cid, active)
+        res["drop_in_latency"] = drop_in_latency(lk, cells, theta_h, rounds.cid_host)
+        # PCIe-inclusive rate of the host-pointer entry point for the whole K-proposal batch
+        # (theta H2D + SS D2H per call): reported beside, never as, `value`.
+        lk.ss_batch(theta_h, rounds.cid_host, act_h)
         h0 = time.perf_counter()
-        for _ in range(3):
-            lk.ss_batch(theta, cid, active)
-        h_el = (time.perf_counter() - h0) / 3
-        res["host_api_pcie_inclusive"] = {"value": n_active / h_el, "unit": "SS evals/s",
-                                          "ms_per_call": h_el * 1e3, "bytes_h2d": int(theta.nbytes + cid.nbytes
-                                                                                    + active.nbytes)}
+        for _ in range(5):
+            lk.ss_batch(theta_h, rounds.cid_host, act_h)
+        h_el = (time.perf_counter() - h0) / 5
+        res["host_api_pcie_inclusive"] = {"value": int(act_h.sum()) / h_el, "unit": "SS evals/s",
+                                          "ms_per_call": h_el * 1e3, "bytes_h2d": int(theta_h.nbytes + rounds.B * 5)}
+    del rounds
     if args.dram_steps > 1:
-        def reduce(x, op):
-            if not distributed:
-                return x
-            t = torch.tensor([float(x)], dtype=torch.float64, device=coll_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
-            return float(t.item())
-
         if distributed:
             dist.barrier()
-        res["end_to_end_dram"] = end_to_end(lk, args.dram_steps, seed=1 + rank, reduce=reduce)
+        e2e = end_to_end(lk, args.dram_steps, seed=1 + rank, reduce=reduce)
+        e2e["workload"] = (f"the metric's named workload (BASELINE config 2): 299-cell TestData, one GPU-resident DRAM "
+                           f"chain per cell, {args.dram_steps} steps, every ssfun evaluation counted")
+        res["end_to_end_dram"] = e2e
         if not args.no_configs:
             res["config3_hierarchical_dram"] = hierarchical_end_to_end(lk, args.dram_steps, seed=3 + rank, reduce=reduce)
     if not args.no_configs:
-        def reduce_k(x, op):
-            if not distributed:
-                return x
-            t = torch.tensor([float(x)], dtype=torch.float64, device=coll_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
-            return float(t.item())
-
         for cfg in (4, 5):
-            res[f"config{cfg}_kernel"] = synthetic_kernel(cfg, rank, world, device_index, 8, args.warmup, args.steps,
-                                                          reduce_k)
+            res[f"config{cfg}_kernel"] = synthetic_kernel(cfg, rank, world, device_index, 8, args.warmup,
+                                                          max(args.steps, 20), reduce)
             if args.synth_dram_steps > 1:
                 res[f"config{cfg}_dram"] = synthetic_end_to_end(cfg, rank, world, device_index, args.synth_dram_steps,
-                                                                reduce_k)
+                                                                reduce)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(cells, theta, cid, active, args.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(cells, theta_h, rounds_cid(cells, args.proposals), act_h, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(res), flush=True)
     lk.close()
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def rounds_cid(cells, K: int) -> np.ndarray:
+    return np.repeat(np.arange(cells.n_cells, dtype=np.int32), K)
 
 
 if __name__ == "__main__":

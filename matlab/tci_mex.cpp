@@ -18,9 +18,13 @@
 //   [ms2, pp7] = tci_mex('forward', h, cell, x, 'raw' | 'interp')
 //   tci_mex('destroy', h)
 // Errors are raised with mexErrMsgIdAndTxt('tci:...'), carrying tci_last_error().
+// Every argument's class and size is checked before a pointer reaches the C ABI. Live contexts
+// are tracked; a handle that this MEX file did not create (or already destroyed) is rejected,
+// and `clear tci_mex` (mexAtExit) destroys the ones still alive.
 #include <stdint.h>
 #include <string.h>
 
+#include <set>
 #include <string>
 #include <vector>
 
@@ -29,9 +33,35 @@
 
 namespace {
 
+std::set<tci_ctx*>& live() {
+  static std::set<tci_ctx*> s;
+  return s;
+}
+
+void destroy_all() {
+  for (tci_ctx* c : live()) tci_destroy(c);
+  live().clear();
+}
+
 tci_ctx* handle_of(const mxArray* a) {
   if (!mxIsUint64(a) || mxGetNumberOfElements(a) != 1) mexErrMsgIdAndTxt("tci:handle", "expected a uint64 handle");
-  return reinterpret_cast<tci_ctx*>(static_cast<uintptr_t>(*static_cast<uint64_t*>(mxGetData(a))));
+  tci_ctx* c = reinterpret_cast<tci_ctx*>(static_cast<uintptr_t>(*static_cast<uint64_t*>(mxGetData(a))));
+  if (!live().count(c)) mexErrMsgIdAndTxt("tci:handle", "not a live tci_mex handle");
+  return c;
+}
+
+// A real double vector of exactly n elements (n < 0: any length).
+const double* doubles(const mxArray* a, long long n, const char* what) {
+  if (!mxIsDouble(a) || mxIsComplex(a) || mxIsSparse(a)) mexErrMsgIdAndTxt("tci:arg", "%s must be real double", what);
+  if (n >= 0 && (long long)mxGetNumberOfElements(a) != n)
+    mexErrMsgIdAndTxt("tci:arg", "%s must have %lld elements", what, n);
+  return mxGetPr(a);
+}
+
+int32_t cell_of(const mxArray* a) {
+  const double c = *doubles(a, 1, "cell");
+  if (!(c >= 1 && c <= 2147483647.0) || c != (double)(int64_t)c) mexErrMsgIdAndTxt("tci:arg", "cell must be a positive integer");
+  return (int32_t)c - 1;
 }
 
 void check(tci_ctx* ctx, int rc, const char* what) {
@@ -76,8 +106,14 @@ void cmd_create(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
       mexErrMsgIdAndTxt("tci:construct", "construct is not defined (GetFluorFromPolPos.m:18)");
   } else if (mxIsStruct(prhs[2])) {
     const char* names[6] = {"MS2_start", "MS2_end", "MS2_loopn", "PP7_start", "PP7_end", "PP7_loopn"};
+    if (mxGetNumberOfElements(prhs[2]) != 1) mexErrMsgIdAndTxt("tci:construct", "construct must be a 1x1 struct");
     for (int k = 0; k < 6; ++k) seg[k] = field_vec(prhs[2], 0, names[k]);
-    cs.L0 = field_vec(prhs[2], 0, "L0").at(0);
+    for (int k = 1; k < 6; ++k)
+      if (seg[k].size() != seg[0].size())
+        mexErrMsgIdAndTxt("tci:construct", "%s and %s must have the same number of segments", names[k], names[0]);
+    const std::vector<double> L0 = field_vec(prhs[2], 0, "L0");
+    if (L0.size() != 1) mexErrMsgIdAndTxt("tci:construct", "L0 must be a scalar");
+    cs.L0 = L0[0];
     cs.n_seg = (int32_t)seg[0].size();
     cs.ms2_start = seg[0].data();
     cs.ms2_end = seg[1].data();
@@ -88,7 +124,7 @@ void cmd_create(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   } else {
     mexErrMsgIdAndTxt("tci:construct", "construct must be a name or a struct");
   }
-  const int device = nrhs > 3 ? (int)mxGetScalar(prhs[3]) : 0;
+  const int device = nrhs > 3 ? (int)*doubles(prhs[3], 1, "device") : 0;
   tci_cells cells{(int64_t)C, off.data(), t.data(), m.data(), p.data()};
   tci_ctx* ctx = nullptr;
   const int rc = tci_create(&cells, &cs, device, &ctx);
@@ -97,7 +133,7 @@ void cmd_create(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     if (ctx) tci_destroy(ctx);
     mexErrMsgIdAndTxt("tci:create", "%s", msg.c_str());
   }
-  plhs[0] = mxCreateNumericMatrix(1, 1, mxUINT64_CLASS, mxREAL);
+  live().insert(ctx);  plhs[0] = mxCreateNumericMatrix(1, 1, mxUINT64_CLASS, mxREAL);
   *static_cast<uint64_t*>(mxGetData(plhs[0])) = static_cast<uint64_t>(reinterpret_cast<uintptr_t>(ctx));
   (void)nlhs;
 }
@@ -105,9 +141,10 @@ void cmd_create(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
 void cmd_ss(mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   if (nrhs != 4) mexErrMsgIdAndTxt("tci:arg", "tci_mex('ss', h, cell, x)");
   tci_ctx* ctx = handle_of(prhs[1]);
-  const int32_t cell = (int32_t)mxGetScalar(prhs[2]) - 1;
+  const int32_t cell = cell_of(prhs[2]);
+  const double* x = doubles(prhs[3], -1, "x");
   double ss = 0;
-  check(ctx, tci_ssfun(ctx, cell, mxGetPr(prhs[3]), (int64_t)mxGetNumberOfElements(prhs[3]), &ss), "tci_ssfun");
+  check(ctx, tci_ssfun(ctx, cell, x, (int64_t)mxGetNumberOfElements(prhs[3]), &ss), "tci_ssfun");
   plhs[0] = mxCreateDoubleScalar(ss);
 }
 
@@ -115,15 +152,29 @@ void cmd_ss_batch(mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   if (nrhs < 4) mexErrMsgIdAndTxt("tci:arg", "tci_mex('ss_batch', h, cells, X[, active])");
   tci_ctx* ctx = handle_of(prhs[1]);
   const mwSize B = mxGetNumberOfElements(prhs[2]);
-  if (mxGetN(prhs[3]) != B) mexErrMsgIdAndTxt("tci:arg", "X must be P x B (one theta per column)");
+  const double* c = doubles(prhs[2], -1, "cells");
+  doubles(prhs[3], -1, "X");
+  if (mxGetNumberOfDimensions(prhs[3]) != 2 || mxGetN(prhs[3]) != B)
+    mexErrMsgIdAndTxt("tci:arg", "X must be P x B (one theta per column)");
   const int64_t P = (int64_t)mxGetM(prhs[3]);  // column-major P x B == row-major B x P
   std::vector<int32_t> cid(B);
-  const double* c = mxGetPr(prhs[2]);
-  for (mwSize b = 0; b < B; ++b) cid[b] = (int32_t)c[b] - 1;
+  for (mwSize b = 0; b < B; ++b) {
+    if (!(c[b] >= 1 && c[b] <= 2147483647.0) || c[b] != (double)(int64_t)c[b])
+      mexErrMsgIdAndTxt("tci:arg", "cells(%d) must be a positive integer", (int)b + 1);
+    cid[b] = (int32_t)c[b] - 1;
+  }
   std::vector<uint8_t> act;
-  if (nrhs > 4) {
-    const mxLogical* a = mxGetLogicals(prhs[4]);
-    act.assign(a, a + B);
+  if (nrhs > 4) {  // logical mask, or a double 0/1 vector (nonzero = active)
+    if (mxGetNumberOfElements(prhs[4]) != B) mexErrMsgIdAndTxt("tci:arg", "active must have B elements");
+    if (mxIsLogical(prhs[4])) {
+      const mxLogical* a = mxGetLogicals(prhs[4]);
+      act.resize(B);
+      for (mwSize b = 0; b < B; ++b) act[b] = a[b] ? 1 : 0;
+    } else {
+      const double* a = doubles(prhs[4], (long long)B, "active");
+      act.resize(B);
+      for (mwSize b = 0; b < B; ++b) act[b] = a[b] != 0.0 ? 1 : 0;
+    }
   }
   plhs[0] = mxCreateDoubleMatrix(B, 1, mxREAL);
   check(ctx, tci_ss_batch(ctx, mxGetPr(prhs[3]), P, cid.data(), act.empty() ? nullptr : act.data(), (int64_t)B,
@@ -133,13 +184,14 @@ void cmd_ss_batch(mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
 void cmd_forward(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   if (nrhs < 4) mexErrMsgIdAndTxt("tci:arg", "tci_mex('forward', h, cell, x[, 'raw'|'interp'])");
   tci_ctx* ctx = handle_of(prhs[1]);
-  const int32_t cell = (int32_t)mxGetScalar(prhs[2]) - 1;
+  const int32_t cell = cell_of(prhs[2]);
+  const double* x = doubles(prhs[3], -1, "x");
   const int mode = (nrhs > 4 && str_of(prhs[4]) == "interp") ? TCI_GRID_INTERP : TCI_GRID_RAW;
   int64_t n = 0;
   check(ctx, tci_cell_points(ctx, cell, &n), "tci_cell_points");
   plhs[0] = mxCreateDoubleMatrix(1, (mwSize)n, mxREAL);
   mxArray* pp7 = mxCreateDoubleMatrix(1, (mwSize)n, mxREAL);
-  check(ctx, tci_forward(ctx, mxGetPr(prhs[3]), (int64_t)mxGetNumberOfElements(prhs[3]), &cell, 1, mode,
+  check(ctx, tci_forward(ctx, x, (int64_t)mxGetNumberOfElements(prhs[3]), &cell, 1, mode,
                          mxGetPr(plhs[0]), mxGetPr(pp7), n), "tci_forward");
   if (nlhs > 1) plhs[1] = pp7; else mxDestroyArray(pp7);
 }
@@ -147,12 +199,23 @@ void cmd_forward(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
 }  // namespace
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+  static bool at_exit = false;
+  if (!at_exit) {
+    mexAtExit(destroy_all);
+    at_exit = true;
+  }
   if (nrhs < 1 || !mxIsChar(prhs[0])) mexErrMsgIdAndTxt("tci:arg", "first argument must be a command");
   const std::string cmd = str_of(prhs[0]);
   if (cmd == "create") cmd_create(nlhs, plhs, nrhs, prhs);
   else if (cmd == "ss") cmd_ss(plhs, nrhs, prhs);
   else if (cmd == "ss_batch") cmd_ss_batch(plhs, nrhs, prhs);
   else if (cmd == "forward") cmd_forward(nlhs, plhs, nrhs, prhs);
-  else if (cmd == "destroy") { if (nrhs > 1) tci_destroy(handle_of(prhs[1])); }
+  else if (cmd == "destroy") {
+    if (nrhs > 1) {
+      tci_ctx* c = handle_of(prhs[1]);
+      live().erase(c);
+      tci_destroy(c);
+    }
+  }
   else mexErrMsgIdAndTxt("tci:arg", "unknown command '%s'", cmd.c_str());
 }

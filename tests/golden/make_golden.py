@@ -23,6 +23,12 @@ that executes nothing from the file):
   ``ss`` is pinned by the forward-model goldens above (bit-exact) and
   statistically by ``s2chain`` (mcmcstat draws 1/s2 ~ Gamma(N/2, 2/SS),
   see tests/test_oracle_golden.py).
+* both result files                                -> ``result_schema.json``
+  the variable names of each file and the field names, in order, of ``MCMCresults``,
+  ``MCMCplot`` and ``MCMCchain`` (TranscriptionCycleMCMC.m:149-157,373-378), so the writer
+  is pinned to the reference's own files, not to a list of our own.
+
+``python tests/golden/make_golden.py --schema`` regenerates only the schema.
 """
 from __future__ import annotations
 
@@ -42,6 +48,28 @@ from oracle import oracle as O  # noqa: E402  (fixture generation is test infras
 
 def _load(name):
     return sio.loadmat(os.path.join(REF, name), squeeze_me=True, struct_as_record=False)
+
+
+def schema():
+    import json
+
+    out = {}
+    for fname, tag in (("28-Oct-2020-TestData.mat", "results_file"), ("28-Oct-2020-TestData_RawChain.mat",
+                                                                        "rawchain_file")):
+        d = _load(fname)
+        out[tag] = {"variables": sorted(k for k in d if not k.startswith("__"))}
+        for k, v in d.items():
+            if k.startswith("__") or not hasattr(np.atleast_1d(v)[0], "_fieldnames"):
+                continue
+            out[tag][k] = list(np.atleast_1d(v)[0]._fieldnames)
+    res = _load("28-Oct-2020-TestData.mat")["MCMCresults"]
+    out["results_file"]["ApprovedFits_values"] = sorted({int(r.ApprovedFits) for r in res})
+    ci = [int(r.cell_index) for r in res]
+    out["results_file"]["n_entries"] = len(ci)
+    out["results_file"]["cell_index_is_1_to_n"] = ci == list(range(1, len(ci) + 1))
+    with open(os.path.join(HERE, "result_schema.json"), "w") as f:
+        json.dump(out, f, indent=1)
+        f.write("\n")
 
 
 def main():
@@ -99,4 +127,6 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--schema" not in sys.argv:
+        main()
+    schema()

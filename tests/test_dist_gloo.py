@@ -26,7 +26,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cells = testdata()
-    b = shard_bounds(cell_weights(cells.lengths), world)
+    b = shard_bounds(cell_weights(cells), world)
     lo, hi = int(b[rank]), int(b[rank + 1])
     # per-cell "result" rows: (cell index, N, sum of finite data) -- deterministic stand-in
     local = np.array([[c, cells.lengths[c], np.nansum(cells.cell(c)[1])] for c in range(lo, hi)])
@@ -73,7 +73,7 @@ def _pack_worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cells = testdata()
-    b = shard_bounds(cell_weights(cells.lengths), world)
+    b = shard_bounds(cell_weights(cells), world)
     fr = _fake_fit(cells, range(int(b[rank]), int(b[rank + 1])))
     rows = gather_rows(pack_results(fr, int(cells.lengths.max())))
     if rank == 0:

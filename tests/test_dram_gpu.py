@@ -316,9 +316,17 @@ def test_chain_keys_let_a_shard_reproduce_the_full_run(lk, engine):
     np.testing.assert_array_equal(d0.chain, d1.chain)
 
 
-def _sharded_worker(rank, world, port, q):
+def _previous_for_shards():
+    """A hierarchical-fit input over all 299 cells with gaps and curation flags (by cell_index)."""
+    from transcriptioncycleinference_amd.mcmc import PreviousFit
+
+    return {c + 1: PreviousFit(1.0 + (c % 17) * 0.1, c % 3 - 1) for c in range(299) if c % 11 != 5}
+
+
+def _sharded_worker(rank, world, port, q, backend="gloo", hierarchical=False):
     import os
 
+    import torch
     import torch.distributed as dist
 
     from transcriptioncycleinference_amd import Likelihood, testdata
@@ -326,26 +334,27 @@ def _sharded_worker(rank, world, port, q):
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL, as on a multi-GPU node (here world 1 on this GPU)
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        dev = "cuda:0"
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = None
     cells = testdata()
+    kw = dict(v0=_previous_for_shards()) if hierarchical else {}
     with Likelihood(cells, "P2P-MS2v5-LacZ-PP7v4", device=0) as L:
-        fr = fit_sharded(L, n_steps=400, n_burn=150, seed=4)
+        fr = fit_sharded(L, device=dev, n_steps=400, n_burn=150, seed=4, **kw)
     if rank == 0:
         q.put(pack_results(fr, int(cells.lengths.max())))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_sharded_fit_world2_equals_the_one_gpu_fit(lk):
-    """parallel.fit_sharded over 2 ranks (gloo, both on this GPU; RCCL on a multi-GPU node): each
-    rank fits its cell range, one all-gather assembles MCMCresults/MCMCplot -- equal bitwise to
-    fitting every cell in one process."""
+def _run_sharded(world, backend, hierarchical):
     import socket
 
     import torch.multiprocessing as mp
-
-    from transcriptioncycleinference_amd.mcmc import fit
-    from transcriptioncycleinference_amd.parallel import pack_results
 
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -353,16 +362,91 @@ def test_sharded_fit_world2_equals_the_one_gpu_fit(lk):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, backend, hierarchical))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    want = pack_results(fit(lk, n_steps=400, n_burn=150, seed=4), int(lk.cells.lengths.max()))
-    assert got.shape == want.shape == (299, want.shape[1])
+    return got
+
+
+@pytest.mark.parametrize("hierarchical", [False, True])
+def test_sharded_fit_world2_equals_the_one_gpu_fit(lk, hierarchical):
+    """parallel.fit_sharded over 2 ranks (gloo, both on this GPU; RCCL on a multi-GPU node): each
+    rank fits its cell range, one all-gather assembles MCMCresults/MCMCplot -- equal bitwise to
+    fitting every cell in one process. The hierarchical case passes loadPrevious inputs with gaps
+    and ApprovedFits over all cells: every rank reads them by cell, not by shard position."""
+    from transcriptioncycleinference_amd.mcmc import fit
+    from transcriptioncycleinference_amd.parallel import pack_results
+
+    got = _run_sharded(2, "gloo", hierarchical)
+    kw = dict(v0=_previous_for_shards()) if hierarchical else {}
+    want = pack_results(fit(lk, n_steps=400, n_burn=150, seed=4, **kw), int(lk.cells.lengths.max()))
+    n = 299 - (len(range(5, 299, 11)) if hierarchical else 0)
+    assert got.shape == want.shape == (n, want.shape[1])
     np.testing.assert_array_equal(got, want)
+    if hierarchical:
+        prev = _previous_for_shards()
+        for row in got:
+            p = prev[int(row[0])]
+            assert row[1] == p.ApprovedFits and abs(row[4] - p.mean_v) <= 1e-5 + 1e-12
+
+
+def test_sharded_fit_over_rccl_world1(lk):
+    """The RCCL branch of parallel.fit_sharded / gather_rows on hardware: backend 'nccl' (RCCL)
+    with device_id, world size 1 (the 8-GPU run is the driver's): equal bitwise to the plain fit."""
+    from transcriptioncycleinference_amd.mcmc import fit
+    from transcriptioncycleinference_amd.parallel import pack_results
+
+    got = _run_sharded(1, "nccl", True)
+    want = pack_results(fit(lk, n_steps=400, n_burn=150, seed=4, v0=_previous_for_shards()),
+                        int(lk.cells.lengths.max()))
+    np.testing.assert_array_equal(got, want)
+
+
+def test_config3_hierarchical_fit_from_a_results_file(lk, tmp_path, means, c_oracle, construct):
+    """BASELINE config 3 at full size, through the file: a results file in the reference's schema
+    holding the reference's own MCMCresults.mean_v (28-Oct-2020-TestData.mat, tests/golden) with
+    two entries removed and curation flags set, read by load_previous, then the 299-cell fixed-v
+    fit (TranscriptionCycleMCMC.m:84-107,193-198,218,236-237,345-350). Checks: cells missing from
+    the file are skipped and pruned, v stays within v0 +- 1e-5, ApprovedFits is carried, and the
+    SS at every chain's final state equals the oracle's."""
+    from transcriptioncycleinference_amd.mcmc import RESULT_FIELDS, FitResult, fit, load_previous, save_results
+
+    cl = lk.cells
+    v_ref = np.array([r[0] for r in means["rows"]])
+    drop = {17, 230}                                        # 1-based cell_index missing from the file
+    res, plots = [], []
+    for c in range(cl.n_cells):
+        if c + 1 in drop:
+            continue
+        n = int(cl.lengths[c])
+        r = {f: 0.0 for f in RESULT_FIELDS}
+        r.update(mean_v=float(v_ref[c]), mean_dR=np.zeros(n), sigma_dR=np.zeros(n), cell_index=c + 1,
+                 ApprovedFits=(1 if c % 4 == 0 else -1 if c % 4 == 1 else 0))
+        res.append(r)
+        t, m, p = cl.cell(c)
+        plots.append({"t_plot": t, "MS2_plot": m, "PP7_plot": p, "simMS2": m, "simPP7": p})
+    path = save_results(FitResult("InitialRise", res, plots, [{} for _ in res], np.zeros(len(res)), 0, 0.0),
+                        str(tmp_path), date="28-Oct-2020")[0]
+    fr = fit(lk, n_steps=2000, n_burn=500, seed=9, v0=load_previous(path))
+    ci = [r["cell_index"] for r in fr.MCMCresults]
+    assert ci == [c + 1 for c in range(cl.n_cells) if c + 1 not in drop]
+    for r in fr.MCMCresults:
+        c = r["cell_index"] - 1
+        assert abs(r["mean_v"] - v_ref[c]) <= 1e-5 + 1e-12
+        assert r["ApprovedFits"] == (1 if c % 4 == 0 else -1 if c % 4 == 1 else 0)
+        assert np.isfinite(r["mean_sigma"]) and np.all(np.isfinite(r["mean_dR"]))
+    assert np.all(np.abs(fr.final_theta[:, 0] - v_ref[fr.cell_index]) <= 1e-5 + 1e-12)
+    cid = fr.cell_index.astype(np.int32)
+    ss = lk.ss_batch(fr.final_theta, cid)
+    want, st = c_oracle.ss_batch(cl.offsets, cl.t, cl.ms2, cl.pp7, construct, fr.final_theta, cid)
+    assert np.all(st == 0)
+    np.testing.assert_allclose(ss, want, rtol=1e-10)
+    assert np.median(fr.accept_rate) > 0.01
 
 
 @pytest.fixture(scope="module")

@@ -138,13 +138,32 @@ def test_missing_library_fails_loudly(tmp_path):
         _lib.load(str(tmp_path / "libtci.so"))
 
 
+def _schema():
+    import json
+
+    with open(os.path.join(GOLDEN, "result_schema.json")) as f:
+        return json.load(f)
+
+
+def test_result_field_lists_are_the_reference_files_own():
+    """RESULT/PLOT/CHAIN_FIELDS equal, in order, the field lists of the reference's own result files
+    (28-Oct-2020-TestData*.mat, extracted by tests/golden/make_golden.py --schema)."""
+    from transcriptioncycleinference_amd.mcmc import CHAIN_FIELDS, PLOT_FIELDS, RESULT_FIELDS
+
+    sc = _schema()
+    assert list(RESULT_FIELDS) == sc["results_file"]["MCMCresults"]
+    assert list(PLOT_FIELDS) == sc["results_file"]["MCMCplot"]
+    assert list(CHAIN_FIELDS) == sc["rawchain_file"]["MCMCchain"]
+
+
 def test_result_files_match_reference_schema(tmp_path, cells):
-    """MCMCresults/MCMCplot/MCMCchain field sets and file names (TranscriptionCycleMCMC.m:149-157,373-378)."""
+    """The two files the writer makes hold the variables and struct fields (in order) of the
+    reference's own files (TranscriptionCycleMCMC.m:149-157,373-378; tests/golden/result_schema.json)."""
     import scipy.io as sio
 
-    from transcriptioncycleinference_amd.mcmc import (CHAIN_FIELDS, PLOT_FIELDS, RESULT_FIELDS, FitResult,
-                                                      save_results)
+    from transcriptioncycleinference_amd.mcmc import CHAIN_FIELDS, RESULT_FIELDS, FitResult, save_results
 
+    sc = _schema()
     n = int(cells.lengths[0])
     t, m, p = cells.cell(0)
     res = {f: 1.0 for f in RESULT_FIELDS}
@@ -156,10 +175,124 @@ def test_result_files_match_reference_schema(tmp_path, cells):
     a, b = save_results(fr, str(tmp_path), date="28-Oct-2020")
     assert a.endswith("28-Oct-2020-TestData.mat") and b.endswith("28-Oct-2020-TestData_RawChain.mat")
     d = sio.loadmat(a, struct_as_record=False, squeeze_me=True)
-    assert set(d["MCMCresults"]._fieldnames) == set(RESULT_FIELDS)
-    assert set(d["MCMCplot"]._fieldnames) == set(PLOT_FIELDS)
-    raw = sio.loadmat(b, struct_as_record=False, squeeze_me=True)["MCMCchain"]
-    assert set(raw._fieldnames) == set(CHAIN_FIELDS) and raw.dR_chain.shape == (5, n)
+    assert sorted(k for k in d if not k.startswith("__")) == sc["results_file"]["variables"]
+    assert list(d["MCMCresults"]._fieldnames) == sc["results_file"]["MCMCresults"]
+    assert list(d["MCMCplot"]._fieldnames) == sc["results_file"]["MCMCplot"]
+    assert d["DatasetName"] == "TestData"
+    raw = sio.loadmat(b, struct_as_record=False, squeeze_me=True)
+    assert sorted(k for k in raw if not k.startswith("__")) == sc["rawchain_file"]["variables"]
+    assert list(raw["MCMCchain"]._fieldnames) == sc["rawchain_file"]["MCMCchain"]
+    assert raw["MCMCchain"].dR_chain.shape == (5, n)
+
+
+def _previous_file(tmp_path, cells, entries):
+    """A results file in the reference's schema holding MCMCresults entries
+    {cell_index: (mean_v, ApprovedFits)} (mean_v None -> MATLAB [])."""
+    from transcriptioncycleinference_amd.mcmc import RESULT_FIELDS, FitResult, save_results
+
+    res, plots = [], []
+    for ci, (v, ap) in entries.items():
+        n = int(cells.lengths[ci - 1])
+        r = {f: 0.5 for f in RESULT_FIELDS}
+        r.update(mean_v=np.zeros((0, 0)) if v is None else v, mean_dR=np.zeros(n), sigma_dR=np.zeros(n),
+                 cell_index=ci, ApprovedFits=ap)
+        res.append(r)
+        t, m, p = cells.cell(ci - 1)
+        plots.append({"t_plot": t, "MS2_plot": m, "PP7_plot": p, "simMS2": m, "simPP7": p})
+    fr = FitResult("Prev", res, plots, [{} for _ in res], np.zeros(len(res)), 0, 0.0)
+    return save_results(fr, str(tmp_path), date="01-Jan-2021")[0]
+
+
+def test_load_previous_keys_by_cell_index_and_skips_gaps(tmp_path, cells):
+    """loadPrevious (TranscriptionCycleMCMC.m:84-107,193-198,345-350): each cell takes the mean_v of
+    the entry whose cell_index matches it; cells with no entry, or an empty mean_v, are skipped;
+    ApprovedFits is carried over. Entries out of order and with gaps, read by cell, never by position."""
+    from transcriptioncycleinference_amd.mcmc import PreviousFit, load_previous, load_previous_v, plan_fit
+
+    entries = {5: (2.5, 1), 1: (1.25, 0), 2: (None, 1), 4: (1.75, -1), 7: (2.0, 1)}   # 3 and 6 missing
+    path = _previous_file(tmp_path, cells, entries)
+    prev = load_previous(path)
+    assert set(prev) == {1, 2, 4, 5, 7}
+    assert prev[5] == PreviousFit(2.5, 1) and prev[4] == PreviousFit(1.75, -1) and prev[2].mean_v is None
+    assert load_previous_v(path) == {1: 1.25, 4: 1.75, 5: 2.5, 7: 2.0}
+    for ids in (range(8), [4, 5, 6, 3]):          # the whole dataset, and one shard of it
+        plan = plan_fit(cells, list(ids), seed=3, v0=prev)
+        want = [c for c in ids if c + 1 in (1, 4, 5, 7)]
+        assert plan.cells == want
+        for k, c in enumerate(plan.cells):
+            v = entries[c + 1][0]
+            assert plan.x0[k, 0] == v
+            assert plan.lower[k, 0] == v - 1e-5 and plan.upper[k, 0] == v + 1e-5 and plan.qcov_diag[k, 0] == 1e-7
+            assert plan.approved[k] == entries[c + 1][1]
+    # the mean_v-only mapping, and an explicit ApprovedFits override by cell_index
+    plan = plan_fit(cells, range(8), seed=3, v0=load_previous_v(path), approved={5: 7})
+    assert plan.cells == [0, 3, 4, 6] and plan.approved == [0, 0, 7, 0]
+    # a sequence over ALL cells is read by 0-based cell index (also inside a shard)
+    seq = [None, 1.5, float("nan"), 2.0, None, None]
+    plan = plan_fit(cells, [3, 1, 2], seed=3, v0=seq)
+    assert plan.cells == [3, 1] and list(plan.x0[:, 0]) == [2.0, 1.5]
+    # x0 of a cell does not depend on which other cells are fitted (keyed by cell)
+    a = plan_fit(cells, [3], seed=3, v0=seq)
+    np.testing.assert_array_equal(a.x0[0], plan.x0[0, :a.x0.shape[1]])
+
+
+class _FakeLk:
+    """Stands in for a Likelihood on CPU: fit()'s host logic only (the sampler is monkeypatched)."""
+
+    def __init__(self, cells):
+        self.cells = cells
+
+    def forward(self, theta, cid, grid="raw"):
+        n = theta.shape[1]
+        return np.zeros((len(cid), n)), np.zeros((len(cid), n))
+
+
+def test_fit_with_load_previous_end_to_end_host_logic(tmp_path, cells, monkeypatch):
+    """The documented call fit(lk, v0=load_previous(path)) builds one chain per cell found in the
+    file, at v0 +- 1e-5, carries ApprovedFits into MCMCresults, prunes the rest, and leaves the
+    caller's DramOptions untouched (the sampler itself is stubbed: it runs on the GPU)."""
+    from transcriptioncycleinference_amd import mcmc
+
+    seen = {}
+
+    def fake_dram_run(lk, cell_id, x0, lo, hi, mu, sg, J0, s20, o, want_qcov=False, chain_keys=None):
+        seen.update(cell_id=cell_id.copy(), lo=lo.copy(), hi=hi.copy(), opts=o, keys=chain_keys.copy())
+        n, ld = x0.shape
+        z = np.zeros((n, ld))
+        return mcmc.DramResult(x0.copy(), z, x0.copy(), np.ones(n), z[:, 0], np.full(n, 0.3),
+                               np.ones(n, np.int64), None, None, 1.0)
+
+    monkeypatch.setattr(mcmc, "dram_run", fake_dram_run)
+    path = _previous_file(tmp_path, cells, {2: (1.5, 1), 4: (2.25, 0), 9: (1.0, -1)})
+    opts = mcmc.DramOptions(engine="walk")
+    before = dict(vars(opts))
+    sub = cells.subset(range(10))
+    fr = mcmc.fit(_FakeLk(sub), n_steps=50, n_burn=10, seed=1, v0=mcmc.load_previous(path), opts=opts)
+    assert vars(opts) == before
+    assert seen["opts"].engine == "walk" and seen["opts"].n_steps == 50
+    assert list(seen["cell_id"]) == [1, 3, 8] and list(seen["keys"]) == [1, 3, 8]
+    np.testing.assert_array_equal(seen["lo"][:, 0], np.array([1.5, 2.25, 1.0]) - 1e-5)
+    assert [r["cell_index"] for r in fr.MCMCresults] == [2, 4, 9]
+    assert [r["ApprovedFits"] for r in fr.MCMCresults] == [1, 0, -1]
+    assert [r["mean_v"] for r in fr.MCMCresults] == [1.5, 2.25, 1.0]
+    # a results file written from this fit can seed the next round (the reference's hierarchy)
+    a, _ = mcmc.save_results(fr, str(tmp_path / ".."), date="02-Jan-2021")
+    assert {c: (p.mean_v, p.ApprovedFits) for c, p in mcmc.load_previous(a).items()} == \
+        {2: (1.5, 1), 4: (2.25, 0), 9: (1.0, -1)}
+
+
+def test_cell_weights_follow_rows_times_window(cells):
+    """Shard weights ~ N_c x W_c: W_c = (L0 + tau v)/(v d_c) at the prior means."""
+    from transcriptioncycleinference_amd.parallel import cell_weights
+
+    w = cell_weights(cells)
+    for c in (0, 17, 298):
+        t = cells.cell(c)[0]
+        n = len(t)
+        d = (t[-1] - t[0]) / (n - 1)
+        assert w[c] == pytest.approx(n * min((6.626 + 2.0 * 2.0) / (2.0 * d), n))
+    wv = cell_weights(cells, v0={1: 4.0})   # a faster previous rate: shorter window
+    assert wv[0] < w[0] and np.all(wv[1:] == w[1:])
 
 
 def test_cell_setup_matches_reference_initialisation():

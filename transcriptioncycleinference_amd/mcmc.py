@@ -17,11 +17,12 @@ fit reproduces the reference's *distribution*, not its exact draws.
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
 import datetime
 import math
 import os
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Mapping, Optional, Sequence
 
 import numpy as np
 
@@ -148,35 +149,73 @@ class FitResult:
     n_evals: int
     elapsed_ms: float
     cell_index: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
+    final_theta: Optional[np.ndarray] = None   # last chain row per fitted cell (padded), mcmcstat results.theta
 
 
-def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 50.0, seed: int = 0,
-        v0: Optional[Sequence[Optional[float]]] = None, approved: Optional[Sequence[int]] = None,
-        thin: int = 0, cells: Optional[Sequence[int]] = None, opts: Optional[DramOptions] = None) -> FitResult:
-    """``TranscriptionCycleMCMC`` for one dataset on the GPU: one DRAM chain per cell.
+@dataclass
+class PreviousFit:
+    """One ``MCMCresults`` entry of an earlier fit as ``loadPrevious`` keeps it
+    (TranscriptionCycleMCMC.m:100-104): the elongation rate and the curation flag."""
 
-    ``lk``: a ``Likelihood`` holding the (truncated) cells. ``v0``: per-cell elongation rates of a
-    previous fit (loadPrevious, :193-198); cells whose v0 is None/NaN are skipped (``continue``,
-    :196-198) and pruned from the outputs (:359-369). ``thin``: keep every thin-th raw chain row
-    in ``MCMCchain`` (the reference keeps all rows from n_burn, :276-283 -- ~193 MB/cell at 200k
-    steps; thin=1 reproduces that). ``cells``: fit only these cell indices (a shard).
+    mean_v: Optional[float]
+    ApprovedFits: int = 0
 
-    Everything random is keyed by the cell index -- x0 by ``default_rng([seed, cell])``, the chain
-    by RNG stream ``cell`` -- so fitting a subset of the cells (one GPU's shard,
-    :func:`parallel.fit_sharded`) reproduces those cells' results of the full fit bit for bit."""
-    cl: Cells = lk.cells
-    ids = list(range(cl.n_cells)) if cells is None else [int(c) for c in cells]
-    rows, keep = [], []
-    for k, c in enumerate(ids):
+
+def _per_cell(values, c: int):
+    """Value for 0-based cell ``c`` of a per-cell input: a mapping keyed by the reference's
+    1-based ``cell_index`` (what :func:`load_previous` returns), or a sequence over every cell
+    of the dataset (0-based). Missing from a mapping -> None."""
+    if values is None:
+        return None
+    if isinstance(values, Mapping):
+        return values.get(c + 1)
+    return values[c]
+
+
+@dataclass
+class FitPlan:
+    """Per-chain inputs of one fit (TranscriptionCycleMCMC.m:193-255), rows padded to ``ld``."""
+
+    cells: List[int]          # 0-based cell indices that get a chain (skipped cells removed, :196-198)
+    x0: np.ndarray
+    lower: np.ndarray
+    upper: np.ndarray
+    prior_mu: np.ndarray
+    prior_sig: np.ndarray
+    qcov_diag: np.ndarray
+    approved: List[int]       # MCMCresults.ApprovedFits per fitted cell (:345-350)
+
+
+def plan_fit(cl: Cells, ids: Sequence[int], seed: int, ratePriorWidth: float = 50.0, v0=None,
+             approved=None) -> FitPlan:
+    """The parfor body's per-cell setup for the cells ``ids`` (host only, no GPU).
+
+    ``v0`` (loadPrevious, :193-198) and ``approved`` are per-cell inputs read by cell, never by
+    position in ``ids``: a mapping keyed by 1-based ``cell_index`` (:194 matches
+    ``[MCMCresults.cell_index] == cellNum``) or a sequence over all cells. A ``PreviousFit`` value
+    carries both. A cell with no previous entry, or an empty/NaN ``mean_v``, is skipped
+    (``continue``, :196-198) and so pruned from the outputs (:359-369). ``ApprovedFits`` is the
+    previous fit's when v0 came from one (:345-347) unless ``approved`` overrides it; 0 otherwise
+    (:349)."""
+    rows, keep, appr = [], [], []
+    for c in ids:
+        c = int(c)
         t = cl.cell(c)[0]
-        vv = None if v0 is None else v0[k]
-        if v0 is not None and (vv is None or not np.isfinite(vv)):
+        prev = _per_cell(v0, c)
+        a = 0
+        if isinstance(prev, PreviousFit):
+            a = int(prev.ApprovedFits)
+            prev = prev.mean_v
+        if v0 is not None and (prev is None or np.size(prev) != 1 or not np.isfinite(float(prev))):
             continue
+        ap = _per_cell(approved, c)
+        if ap is not None:
+            a = int(ap)
+        vv = None if v0 is None else float(prev)
         rows.append(cell_setup(t, np.random.default_rng([int(seed), c]), ratePriorWidth, vv))
         keep.append(c)
-    if not keep:
-        return FitResult(cl.name, [], [], [], np.zeros(0), 0, 0.0)
-    ld = max(len(r[0]) for r in rows)
+        appr.append(a)
+    ld = max((len(r[0]) for r in rows), default=7)
 
     def stack(i, fill):
         out = np.full((len(rows), ld), fill, np.float64)
@@ -184,12 +223,38 @@ def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 5
             out[k, :len(r[i])] = r[i]
         return out
 
-    x0, lo, hi, mu, sg, J0 = (stack(0, 0.0), stack(1, -np.inf), stack(2, np.inf), stack(3, 0.0), stack(4, np.inf),
-                              stack(5, 1.0))
-    o = opts or DramOptions()
+    return FitPlan(keep, stack(0, 0.0), stack(1, -np.inf), stack(2, np.inf), stack(3, 0.0), stack(4, np.inf),
+                   stack(5, 1.0), appr)
+
+
+def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 50.0, seed: int = 0,
+        v0=None, approved=None, thin: int = 0, cells: Optional[Sequence[int]] = None,
+        opts: Optional[DramOptions] = None) -> FitResult:
+    """``TranscriptionCycleMCMC`` for one dataset on the GPU: one DRAM chain per cell.
+
+    ``lk``: a ``Likelihood`` holding the (truncated) cells. ``v0``: the previous fit of a
+    hierarchical run (loadPrevious): ``load_previous(path)`` (cell_index -> PreviousFit), a
+    mapping cell_index -> mean_v, or a sequence of rates over ALL cells (None/NaN = no entry).
+    Cells without an entry are skipped (``continue``, :196-198) and pruned from the outputs
+    (:359-369); see :func:`plan_fit`. ``thin``: keep every thin-th raw chain row in ``MCMCchain``
+    (the reference keeps all rows from n_burn, :276-283 -- ~193 MB/cell at 200k steps; thin=1
+    reproduces that). ``cells``: fit only these cell indices (a shard).
+
+    Everything random is keyed by the cell index -- x0 by ``default_rng([seed, cell])``, the chain
+    by RNG stream ``cell`` -- so fitting a subset of the cells (one GPU's shard,
+    :func:`parallel.fit_sharded`) reproduces those cells' results of the full fit bit for bit."""
+    cl: Cells = lk.cells
+    ids = list(range(cl.n_cells)) if cells is None else [int(c) for c in cells]
+    plan = plan_fit(cl, ids, seed, ratePriorWidth, v0, approved)
+    keep = plan.cells
+    if not keep:
+        return FitResult(cl.name, [], [], [], np.zeros(0), 0, 0.0)
+    # a private copy: the caller's options object is never modified
+    o = dataclasses.replace(opts) if opts is not None else DramOptions()
     o.n_steps, o.burnintime, o.stats_from, o.thin = int(n_steps), int(n_burn), int(max(n_burn, 1)), int(thin)
     o.seed = int(seed) * 1000003 + 20201028
-    res = dram_run(lk, np.array(keep, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, chain_keys=np.array(keep, np.int64))
+    res = dram_run(lk, np.array(keep, np.int32), plan.x0, plan.lower, plan.upper, plan.prior_mu, plan.prior_sig,
+                   plan.qcov_diag, 1.0, o, chain_keys=np.array(keep, np.int64))
     # forward model at the means on the raw times (:307-309)
     ms2, pp7 = lk.forward(res.mean, np.array(keep, np.int32), grid="raw")
     results, plots, chains = [], [], []
@@ -204,7 +269,7 @@ def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 5
         r["mean_dR"], r["sigma_dR"] = mean[7:].copy(), std[7:].copy()
         r["mean_sigma"], r["sigma_sigma"] = float(res.sigma_mean[k]), float(res.sigma_std[k])
         r["cell_index"] = c + 1                                               # :343 (1-based)
-        r["ApprovedFits"] = int(approved[ids.index(c)]) if approved is not None else 0   # :345-350
+        r["ApprovedFits"] = plan.approved[k]                                  # :345-350
         results.append({f: r[f] for f in RESULT_FIELDS})
         plots.append({"t_plot": t.copy(), "MS2_plot": m.copy(), "PP7_plot": p.copy(),
                       "simMS2": ms2[k, :n].copy(), "simPP7": pp7[k, :n].copy()})
@@ -220,7 +285,7 @@ def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 5
             ch["s2chain"] = res.s2chain[:, k].copy()  # s2chain is not sliced by n_burn (:323)
         chains.append(ch)
     return FitResult(cl.name, results, plots, chains, res.accept_rate, int(res.n_evals.sum()), res.elapsed_ms,
-                     np.array(keep, np.int64))
+                     np.array(keep, np.int64), res.final_theta)
 
 
 # ---------------------------------------------------------------------------
@@ -259,15 +324,30 @@ def save_results(fit_result: FitResult, save_loc: str = ".", date: Optional[str]
     return base + ".mat", base + "_RawChain.mat"
 
 
-def load_previous_v(results_path: str) -> Dict[int, float]:
-    """``loadPrevious`` (hierarchical fit, :84-107,193-198): cell_index -> mean_v of an earlier
-    result file (read with scipy.io.loadmat: a data reader, nothing executes)."""
+def load_previous(results_path: str) -> Dict[int, PreviousFit]:
+    """``loadPrevious`` (hierarchical fit, TranscriptionCycleMCMC.m:84-107): the ``MCMCresults``
+    of an earlier result file as ``cell_index -> PreviousFit(mean_v, ApprovedFits)``. The fit
+    looks each cell up by ``cell_index`` (:194), so cells missing from the file (pruned there,
+    :359-369) are skipped, never shifted. A repeated cell_index keeps its first entry (MATLAB's
+    ``v0 = MCMCresults(cellToload).mean_v`` takes the first of a comma list). Read with
+    scipy.io.loadmat: a data reader, nothing executes."""
     import scipy.io as sio
 
     d = sio.loadmat(results_path, squeeze_me=True, struct_as_record=False)
-    out = {}
+    out: Dict[int, PreviousFit] = {}
     for r in np.atleast_1d(d["MCMCresults"]):
+        ci = getattr(r, "cell_index", None)
+        if ci is None or np.size(ci) != 1:
+            continue
         v = getattr(r, "mean_v", None)
-        if v is not None and np.size(v) == 1 and math.isfinite(float(v)):
-            out[int(r.cell_index)] = float(v)
+        v = float(v) if v is not None and np.size(v) == 1 else None   # [] -> skipped at :196
+        a = getattr(r, "ApprovedFits", 0)
+        a = int(a) if np.size(a) == 1 else 0
+        out.setdefault(int(ci), PreviousFit(v, a))
     return out
+
+
+def load_previous_v(results_path: str) -> Dict[int, float]:
+    """``cell_index -> mean_v`` of an earlier result file (entries with a usable rate only)."""
+    return {c: p.mean_v for c, p in load_previous(results_path).items()
+            if p.mean_v is not None and math.isfinite(p.mean_v)}

@@ -34,9 +34,32 @@ def shard_bounds(weights: Sequence[float], world: int) -> np.ndarray:
     return np.asarray(bounds, dtype=np.int64)
 
 
-def cell_weights(lengths: Sequence[int]) -> np.ndarray:
-    """Work per cell ~ rows x elongation window; the window is theta-dependent, rows are not."""
-    return np.asarray(lengths, dtype=np.float64)
+# Prior means of the reference's x0 draw (TranscriptionCycleMCMC.m:200-208): v ~ U(1,3), tau ~ U(0,4).
+_V_MEAN, _TAU_MEAN = 2.0, 2.0
+
+
+def cell_weights(cells, L0: float = 6.626, v0=None) -> np.ndarray:
+    """Work per cell ~ N_c x W_c: N_c grid rows, each summing over the cohorts
+    inside the elongation window, W_c = (L0 + tau*v) / (v * d_c) grid steps (capped at N_c) at
+    the prior means of v and tau; d_c = mean(diff(t)) is the cell's grid increment
+    (SumofSquares...m:29). ``v0`` (hierarchical fit, a mapping by 1-based cell_index or a
+    sequence over all cells) replaces the prior mean of v where given."""
+    from .mcmc import PreviousFit, _per_cell
+
+    n = cells.lengths.astype(np.float64)
+    w = np.empty(cells.n_cells)
+    for c in range(cells.n_cells):
+        t = cells.cell(c)[0]
+        v = _V_MEAN
+        p = _per_cell(v0, c)
+        if isinstance(p, PreviousFit):
+            p = p.mean_v
+        if p is not None and np.isfinite(p) and p > 0:
+            v = float(p)
+        d = (t[-1] - t[0]) / (len(t) - 1) if len(t) > 1 else 1.0
+        win = (L0 + _TAU_MEAN * v) / (v * d) if d > 0 else n[c]
+        w[c] = n[c] * min(max(win, 1.0), max(n[c], 1.0))
+    return w
 
 
 def gather_rows(local: np.ndarray, group=None, device: Optional[str] = None) -> np.ndarray:
@@ -118,13 +141,14 @@ def unpack_results(rows: np.ndarray, cells, dataset_name: str, n_evals: int, ela
                      (rows[:, 0].astype(np.int64) - 1))
 
 
-def fit_sharded(lk, group=None, device: Optional[str] = None, v0=None, **fit_kwargs):
+def fit_sharded(lk, group=None, device: Optional[str] = None, v0=None, approved=None, **fit_kwargs):
     """``TranscriptionCycleMCMC`` over ``torch.distributed`` ranks, one GPU each: rank r fits the
     contiguous cell range ``shard_bounds`` gives it (its own GPU-resident DRAM chains), then ONE
     all-gather of the packed per-cell results (RCCL on GPUs, gloo on CPU) gives every rank the
     whole dataset's ``MCMCresults`` / ``MCMCplot``. The chains' randomness is keyed by cell index
     (:func:`mcmc.fit`), so the gathered results equal a one-GPU fit of all cells bit for bit.
-    ``v0``: per-cell previous rates over ALL cells (hierarchical fit), sliced per shard."""
+    ``v0`` / ``approved``: per-cell inputs over ALL cells (by 1-based cell_index in a mapping, or
+    0-based in a sequence); ``fit`` reads them by cell, so every shard passes them unchanged."""
     import torch
     import torch.distributed as dist
 
@@ -132,10 +156,9 @@ def fit_sharded(lk, group=None, device: Optional[str] = None, v0=None, **fit_kwa
 
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     cl = lk.cells
-    b = shard_bounds(cell_weights(cl.lengths), world)
+    b = shard_bounds(cell_weights(cl, lk.construct.L0, v0), world)
     ids = list(range(int(b[rank]), int(b[rank + 1])))
-    vv = None if v0 is None else [v0[c] for c in ids]
-    fr = fit(lk, cells=ids, v0=vv, **fit_kwargs) if ids else None
+    fr = fit(lk, cells=ids, v0=v0, approved=approved, **fit_kwargs) if ids else None
     n_max = int(np.max(cl.lengths))
     local = pack_results(fr, n_max) if fr is not None else np.zeros((0, 4 + len(_SCALARS) + 4 * n_max))
     rows = gather_rows(local, group=group, device=device)
