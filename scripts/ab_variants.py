@@ -47,12 +47,15 @@ VARIANTS = {
 }
 
 
-def build(names):
+def build(names, jobs=4):
+    from concurrent.futures import ThreadPoolExecutor
+
     from transcriptioncycleinference_amd.build import build_library
 
     os.makedirs(OUT, exist_ok=True)
-    for n in names:
-        build_library(out=os.path.join(OUT, f"libtci_{n}.so"), defines=VARIANTS[n], verbose=True)
+    todo = [n for n in names if VARIANTS.get(n) is not None]
+    with ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(lambda n: build_library(out=os.path.join(OUT, f"libtci_{n}.so"), defines=VARIANTS[n]), todo))
 
 
 def run(names, rounds, launches, proposals):
@@ -67,7 +70,9 @@ def run(names, rounds, launches, proposals):
     th_d = torch.from_numpy(theta).to(dev)
     cid_d = torch.from_numpy(cid).to(dev)
     act_d = torch.from_numpy(active).to(dev)
-    lks = {n: Likelihood(cells, bench.CONSTRUCT, 0, lib_path=os.path.join(OUT, f"libtci_{n}.so")) for n in names}
+    # "main": the in-tree libtci.so (the shipped build)
+    lks = {n: Likelihood(cells, bench.CONSTRUCT, 0, lib_path=None if n == "main" else os.path.join(OUT, f"libtci_{n}.so"))
+           for n in names}
     outs = {n: torch.empty(len(cid), dtype=torch.float64, device=dev) for n in names}
     st = torch.cuda.current_stream(dev)
     for n in names:  # warm + correctness

@@ -16,7 +16,7 @@ REPO_ROOT = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 SOURCES = [os.path.join(CSRC, "tci_kernels.hip"), os.path.join(CSRC, "tci_dram.hip"), os.path.join(CSRC, "tci_api.cpp")]
 HEADERS = [os.path.join(REPO_ROOT, "include", "tci.h"), os.path.join(CSRC, "tci_internal.h"),
-           os.path.join(CSRC, "tci_dram_internal.h")]
+           os.path.join(CSRC, "tci_dram_internal.h"), os.path.join(CSRC, "tci_eval.h")]
 LIB = os.path.join(PKG_DIR, "libtci.so")
 ARCH = os.environ.get("TCI_OFFLOAD_ARCH", "gfx950")
 

@@ -166,6 +166,19 @@ __device__ __forceinline__ double lane_bcast(double x, int l) {
 
 constexpr int kVec = TCI_MAX_POINTS + 8;
 
+// Acceptance terms shared by every engine (the same expressions, so the same bits):
+//   log of a Metropolis ratio  -0.5*(ss_new - ss_old)/s2 - 0.5*(prior_new - prior_old), with the
+//   division by s2 taken as a product with the precision ip = 1/s2 (computed once per state);
+//   the delayed-rejection test  u2 < alpha13 = l2*q1*(1-alpha32)/(1-alpha12)  as the product form
+//   u2*(1-alpha12) < l2*q1*(1-alpha32)  (stage 2 runs only after a stage-1 rejection, so
+//   alpha12 < 1 there and the two tests agree in exact arithmetic).
+__device__ __forceinline__ double dram_log_ratio(double ss_new, double ss_old, double pr_new, double pr_old, double ip) {
+  return -0.5 * (ss_new - ss_old) * ip - 0.5 * (pr_new - pr_old);
+}
+__device__ __forceinline__ bool dram_dr_accept(double u2, double a12, double a32, double l2, double q1) {
+  return u2 * (1.0 - a12) < l2 * q1 * (1.0 - a32);
+}
+
 // Prior SS sum(((th - mu)./sig).^2) over finite sig (mcmcstat's default priorfun) by ONE wave:
 // lane l sums j = l, l + 64, .. in order, then a fixed xor-shuffle tree. Both engines call this,
 // so the bits agree.
@@ -513,8 +526,7 @@ __global__ __launch_bounds__(kThreads) void k_accept1(DramState st, DramParams p
   bool acc = false;
   if (inb) {
     pr1 = prior_block(y1, st.pmu + c * ld, st.psig + c * ld, P, sm.red);
-    const double e = -0.5 * (st.ss1[c] - st.ss[c]) / st.sigma2[c] - 0.5 * (pr1 - st.prior[c]);
-    a12 = fmin(1.0, exp(e));
+    a12 = fmin(1.0, exp(dram_log_ratio(st.ss1[c], st.ss[c], pr1, st.prior[c], 1.0 / st.sigma2[c])));
     acc = uniform_at(p.seed, st.key[c], step, P_U1) < a12;
   }
   if (acc) {
@@ -553,14 +565,14 @@ __global__ __launch_bounds__(kThreads) void k_accept2(DramState st, DramParams p
     const double pr2 = prior_block(y2, st.pmu + c * ld, st.psig + c * ld, P, sm.red);
     const double s2 = st.sigma2[c], ss2 = st.ss2[c], ss1 = st.ss1[c], a12 = st.a12[c];
     // ss1 = +Inf (stage 1 out of bounds) gives alpha32 = 0, alpha12 = 0
-    const double a32 = fmin(1.0, exp(-0.5 * (ss1 - ss2) / s2 - 0.5 * (st.prior1[c] - pr2)));
-    const double l2 = exp(-0.5 * (ss2 - st.ss[c]) / s2 - 0.5 * (pr2 - st.prior[c]));
+    const double ip = 1.0 / s2;
+    const double a32 = fmin(1.0, exp(dram_log_ratio(ss1, ss2, st.prior1[c], pr2, ip)));
+    const double l2 = exp(dram_log_ratio(ss2, st.ss[c], pr2, st.prior[c], ip));
     draw_normals(p.seed, st.key[c], step, P_NORM1, P, sm.z, threadIdx.x);
     draw_normals(p.seed, st.key[c], step, P_NORM2, P, sm.y, threadIdx.x);
     __syncthreads();
     const double q1 = dr_q1(sm.z, sm.y, 1.0 / p.drscale, P, sm.red);
-    const double a13 = l2 * q1 * (1.0 - a32) / (1.0 - a12);
-    acc2 = uniform_at(p.seed, st.key[c], step, P_U2) < a13;
+    acc2 = dram_dr_accept(uniform_at(p.seed, st.key[c], step, P_U2), a12, a32, l2, q1);
     if (acc2) {
       for (int j = threadIdx.x; j < P; j += kThreads) th[j] = y2[j];
       if (threadIdx.x == 0) {
@@ -890,15 +902,18 @@ __device__ __forceinline__ uint64_t stamp() {
 #endif
 }
 
-// Which waves keep the chain records (window row + column sums + posterior Welford, and the s2
-// statistics): waves that finish their evaluations early have slack before the barrier.
+// Which waves keep the chain records. Both are stage-1 waves: a stage-1 proposal is more often out
+// of bounds (it skips ssfun), so these waves reach the barrier first and have slack before it.
+//   kRecWave: window row + column sums + posterior Welford + thinned rows of the decided rows;
+//   kSigWave: the sigma2 chain (s2 of each decided row, its statistics and thinned rows) and the
+//             precisions 1/s2 the next decisions use.
 #ifndef TCI_REC_WAVE
 #define TCI_REC_WAVE 0
 #endif
-#ifndef TCI_S2_WAVE
-#define TCI_S2_WAVE 1
+#ifndef TCI_SIG_WAVE
+#define TCI_SIG_WAVE 2
 #endif
-constexpr int kRecWave = TCI_REC_WAVE, kS2Wave = TCI_S2_WAVE;
+constexpr int kRecWave = TCI_REC_WAVE, kSigWave = TCI_SIG_WAVE;
 
 template <int RPL, int NSEG>
 __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
@@ -911,13 +926,21 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   // not move, step s+1's evaluations are exactly the ones the sequential sampler would make, and
   // step s+1 is decided in the same round. Decisions, counters and records are those of the
   // step-by-step sampler (and of the batched engine) bit for bit.
+  //
+  // After the barrier only the decisions run: one lane-parallel exp and the compares. Everything
+  // that does not depend on the exchanged values happens before the barrier, on the stage-1
+  // waves (kRecWave, kSigWave), one round late for the records:
+  //   * the precisions the decisions use: 1/s2 of the current state (step s) and, for step s+1
+  //     after an unmoved step s, 1/s2 with s2 = 1/(G_s*(2/ss)) -- both known before the round;
+  //   * the s2 of the rows the previous round decided (1/(G*(2/ss)) of the state after them)
+  //     and the records of those rows.
   constexpr int NJ = RPL + 1;  // vector entries per lane: P = 7 + N <= 64 RPL + 8 <= 64 NJ
   constexpr int EV = eval_lds_doubles<RPL>();
   constexpr int NW = kThreads / 64;
   __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each evaluating wave's tables
   __shared__ double yl[2][NW][64 * NJ];                         // by round parity: each wave's proposal
   __shared__ double xch[2][NW][4];                              // by round parity: ss, prior, in-bounds of each
-  __shared__ double xsc[2][2][5];                               // by round parity: scalar draws of s, s+1
+  __shared__ double xip[2][2];                                  // by round parity: the precisions of steps s, s+1
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -927,12 +950,13 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
   const int stage = w & 1, ahead = w >> 1;                        // this wave's proposal
   const double scale = stage ? 1.0 / p.drscale : 1.0;
-  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], smn[NJ], sm2[NJ], wsv[NJ];
+  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], smn[NJ], sm2[NJ], wsv[NJ], thp[NJ];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
     const int j = lane + 64 * k;
     const bool in = j < P;
     th[k] = in ? st.theta[c * ld + j] : 0.0;
+    thp[k] = th[k];
     lo[k] = in ? st.lower[c * ld + j] : 0.0;
     hi[k] = in ? st.upper[c * ld + j] : 0.0;
     mu[k] = in ? st.pmu[c * ld + j] : 0.0;
@@ -957,11 +981,17 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       e.pt[k] = j <= 64 * RPL ? kp.points[cbase + j] : PointRec{NAN, NAN, NAN, 0, 0};
     }
   }
-  double ss = st.ss[c], prior = st.prior[c], s2 = st.sigma2[c];
-  S2Stats s2a{0.0, 0.0, 0.0};  // held by wave 1
-  if (w == kS2Wave) s2a = S2Stats{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
+  double ss = st.ss[c], prior = st.prior[c];
+  // sigma2 chain (kSigWave): s2 of the last decided row, or its Gamma variate Gl while that s2
+  // (1/(Gl*(2/ss)), ss of the state after the row) is pending; s2 of the first of two rows
+  double s2c = st.sigma2[c], Gl = 0.0, s2first = 0.0;
+  bool gpend = false;
+  S2Stats s2a{0.0, 0.0, 0.0};
+  if (w == kSigWave) s2a = S2Stats{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
   int32_t nacc = st.naccept[c], nrej = st.nrej_win[c];
   int64_t nev = st.nevals[c];
+  int64_t prow = 0;  // rows prow .. prow + padv - 1 were decided by the previous round (records pending);
+  int padv = 0;      // of two, the first did not move the chain (its row is thp)
   // this wave's proposal offsets: rows s + ahead (cur), s + ahead + 1, s + ahead + 2 (prefetched)
   auto load_u = [&](double* u, int64_t row) {
     const double* src = drow + min(row, s_end) * DW + stage * ld;
@@ -975,14 +1005,37 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   int par = 0;
   RowCursor cur;
   cur.init(p, s_begin);
-  uint64_t ph[6] = {0, 0, 0, 0, 0, 0}, t0 = stamp(), t1;
+  // the records of the pending rows (kRecWave: vectors, kSigWave: s2 with x0 = s2 of the last row)
+  auto flush_vec = [&]() {
+    if (padv == 2) {
+      record_vec_reg<NJ>(st, p, c, prow, P, thp, smn, sm2, wsv, lane, cur);
+      cur.next(p);
+    }
+    if (padv >= 1) {
+      record_vec_reg<NJ>(st, p, c, prow + padv - 1, P, th, smn, sm2, wsv, lane, cur);
+      cur.next(p);
+    }
+  };
+  auto flush_s2 = [&](double x0) {
+    if (padv == 2) {
+      if (lane == 0) record_s2_cur(st, p, c, prow, s2first, s2a, cur);
+      cur.next(p);
+    }
+    if (padv >= 1) {
+      if (lane == 0) record_s2_cur(st, p, c, prow + padv - 1, x0, s2a, cur);
+      cur.next(p);
+    }
+  };
+  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = stamp(), t1;
 #define TCI_PHASE(k) \
   if (TCI_CHAIN_PROFILE) { t1 = stamp(); ph[k] += t1 - t0; t0 = t1; }
   for (int64_t s = s_begin; s <= s_end; par ^= 1) {
     const bool has_next = s + 1 <= s_end;
-    // wave 3 fetches the scalar draws of steps s, s+1 (lanes 0-9) while it evaluates
-    double scv = 0.0;
-    if (w == NW - 1 && lane < 10) scv = drow[min(s + lane / 5, s_end) * DW + 2 * ld + lane % 5];
+    // the scalar draws of steps s and s+1 (wave-uniform loads)
+    const double* sc0 = drow + s * DW + 2 * ld;
+    const double* sc1 = drow + min(s + 1, s_end) * DW + 2 * ld;
+    const double Q1a = sc0[D_Q1], U1a = sc0[D_U1], U2a = sc0[D_U2], Ga = sc0[D_G];
+    const double Q1b = sc1[D_Q1], U1b = sc1[D_U1], U2b = sc1[D_U2], Gb = sc1[D_G];
     // ---- this wave's proposal and its bounds (wave vote)
     double y[NJ];
     bool out = false;
@@ -1016,66 +1069,70 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       TCI_PHASE(1)
       pr = wave_prior_reg<NJ>(y, mu, sg, P, lane);
     }
-    TCI_PHASE(2)
     if (lane == 0) {
       xch[par][w][0] = r;
       xch[par][w][1] = pr;
       xch[par][w][2] = inb ? 1.0 : 0.0;
     }
-    if (w == NW - 1 && lane < 10) xsc[par][lane / 5][lane % 5] = scv;
+    if (w == kSigWave) {
+      // lanes 0-2: s2 of the last decided row (pending: 1/(Gl*(2/ss))), after step s unmoved
+      // (1/(G_s*(2/ss))), after step s+1 with step s unmoved (1/(G_s+1*(2/ss))); lanes 0-1 also
+      // the precision of that s2, which the decisions of steps s and s+1 use
+      const double gv = lane == 0 ? Gl : lane == 1 ? Ga : Gb;
+      double x = 1.0 / (gv * (2.0 / ss));
+      if (!p.updatesigma || (lane == 0 && !gpend)) x = s2c;
+      const double ipv = 1.0 / x;
+      if (lane < 2) xip[par][lane] = ipv;
+      const double x0 = lane_bcast(x, 0);
+      flush_s2(x0);
+      s2c = x0;
+      gpend = false;
+      s2first = lane_bcast(x, 1);  // the s2 of row s if it does not move the chain
+    }
+    if (w == kRecWave) flush_vec();
+    if (w == kRecWave) {
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) thp[k] = th[k];  // the state before this round's rows
+    }
+    TCI_PHASE(2)
     __syncthreads();
     TCI_PHASE(3)
     // ---- decisions: step s, then (if the chain did not move) step s+1 from the speculation.
-    // Every transcendental/division the two steps can need is evaluated ONCE, in parallel lanes
-    // (the sequential sampler's exact expressions, per-lane operands), then picked by readlane:
-    //   level 1, lanes 0-5: sigma2 after step s (lanes 0-2: state unchanged / stage-1 / stage-2
-    //            move) and after step s+1 with step s unmoved (lanes 3-5): 1 / (G * (2 / SS));
-    //   level 2, lanes 0-2 (step s) and 3-5 (step s+1, sigma2 = lane 0's): a12, a32, l2;
-    //   level 3, lanes 0/1: a13 = l2 q1 (1 - a32) / (1 - a12) of step s / s+1.
+    // The three exponentials each step can need -- a12, a32, l2 (dram_log_ratio) -- for both
+    // steps are ONE lane-parallel exp (lanes 0-2: step s, 3-5: step s+1), picked by readlane.
     const double* X0 = xch[par][0];
     const double* X1 = xch[par][1];
     const double* X2 = xch[par][2];
     const double* X3 = xch[par][3];
-    const double* SC0 = xsc[par][0];
-    const double* SC1 = xsc[par][1];
     const bool inb1a = X0[2] != 0.0, inb2a = X1[2] != 0.0, inb1b = X2[2] != 0.0, inb2b = X3[2] != 0.0;
     const double pr1a = inb1a ? X0[1] : 0.0, pr2a = inb2a ? X1[1] : 0.0;
     const double pr1b = inb1b ? X2[1] : 0.0, pr2b = inb2b ? X3[1] : 0.0;
     const int h = lane < 3 ? 0 : 1, k3 = lane < 3 ? lane : lane - 3;  // lanes >= 6 compute junk
     const double ssA = h ? X2[0] : X0[0], ssB = h ? X3[0] : X1[0];
-    const double Gh = h ? SC1[D_G] : SC0[D_G];
-    const double s2n = 1.0 / (Gh * (2.0 / (k3 == 0 ? ss : k3 == 1 ? ssA : ssB)));
-    const double s2n0 = lane_bcast(s2n, 0);
-    const double s2u = (h && p.updatesigma) ? s2n0 : s2;  // step s+1 runs at sigma2 after an unmoved step s
     const double prA = h ? pr1b : pr1a, prB = h ? pr2b : pr2a;
+    const double ipu = xip[par][h];
     // one expression, per-lane operands: a12 (k3 = 0), a32 (k3 = 1), l2 (k3 = 2)
     const double eA = k3 == 2 ? ssB : ssA, eB = k3 == 1 ? ssB : ss;
     const double eC = k3 == 2 ? prB : prA, eD = k3 == 1 ? prB : prior;
-    const double ev = exp(-0.5 * (eA - eB) / s2u - 0.5 * (eC - eD));
+    const double ev = exp(dram_log_ratio(eA, eB, eC, eD, ipu));
     const double av = k3 == 2 ? ev : fmin(1.0, ev);
     const double a12a = lane_bcast(av, 0), a32a = lane_bcast(av, 1), l2a = lane_bcast(av, 2);
     const double a12b = lane_bcast(av, 3), a32b = lane_bcast(av, 4), l2b = lane_bcast(av, 5);
-    const double q1h = lane == 0 ? SC0[D_Q1] : SC1[D_Q1];
-    const double l2h = lane == 0 ? l2a : l2b, a32h = lane == 0 ? a32a : a32b, a12h = lane == 0 ? a12a : a12b;
-    const double a13v = l2h * q1h * (1.0 - a32h) / (1.0 - a12h);  // lane 0: step s, lane 1: step s+1
-    const double a13a = lane_bcast(a13v, 0), a13b = lane_bcast(a13v, 1);
-    const double s2_0 = s2n0, s2_1 = lane_bcast(s2n, 1), s2_2 = lane_bcast(s2n, 2);
-    const double s2_3 = lane_bcast(s2n, 3), s2_4 = lane_bcast(s2n, 4), s2_5 = lane_bcast(s2n, 5);
+    TCI_PHASE(4)
     int adv = 0;
     for (int hh = 0; hh < 2; ++hh) {
       if (hh == 1 && !has_next) break;
       const double* x1 = hh ? X2 : X0;
       const double* x2 = hh ? X3 : X1;
-      const double* sc = hh ? SC1 : SC0;
       const bool inb1 = hh ? inb1b : inb1a, inb2 = hh ? inb2b : inb2a;
       bool acc = false, acc2 = false;
       if (inb1) {
         nev += 1;
-        acc = sc[D_U1] < (hh ? a12b : a12a);
+        acc = (hh ? U1b : U1a) < (hh ? a12b : a12a);
       }
       if (!acc && inb2) {
         nev += 1;
-        acc2 = sc[D_U2] < (hh ? a13b : a13a);
+        acc2 = hh ? dram_dr_accept(U2b, a12b, a32b, l2b, Q1b) : dram_dr_accept(U2a, a12a, a32a, l2a, Q1a);
       }
       const bool moved = acc || acc2;
       if (moved) {
@@ -1088,17 +1145,15 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       } else {
         nrej += 1;
       }
-      // sigma2 Gibbs update of this row (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/ss)
-      if (p.updatesigma) s2 = hh ? (acc ? s2_4 : acc2 ? s2_5 : s2_3) : (acc ? s2_1 : acc2 ? s2_2 : s2_0);
-      // the row's records
-      const int64_t row = s + hh;
-      if (w == kRecWave) record_vec_reg<NJ>(st, p, c, row, P, th, smn, sm2, wsv, lane, cur);
-      if (w == kS2Wave && lane == 0) record_s2_cur(st, p, c, row, s2, s2a, cur);
-      cur.next(p);
       adv = hh + 1;
       if (moved) break;  // step s+1 must be re-proposed around the new state
     }
-    TCI_PHASE(4)
+    // the rows s .. s + adv - 1 are recorded next round (s2 of the last: 1/(G*(2/ss)), ss after it)
+    prow = s;
+    padv = adv;
+    Gl = adv == 1 ? Ga : Gb;
+    gpend = p.updatesigma != 0;
+    TCI_PHASE(6)
     // ---- advance the proposal offsets by adv rows
     if (adv == 1) {
 #pragma unroll
@@ -1125,9 +1180,11 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   }
 #else
   if (TCI_CHAIN_PROFILE && w == 0 && lane == 0 && st.prof != nullptr)
-    for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long*)&st.prof[k], (unsigned long long)ph[k]);
+    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&st.prof[k], (unsigned long long)ph[k]);
 #endif
+  // the last round's rows
   if (w == kRecWave) {
+    flush_vec();
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
       const int j = lane + 64 * k;
@@ -1141,17 +1198,21 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     if (lane == 0) {
       st.ss[c] = ss;
       st.prior[c] = prior;
-      st.sigma2[c] = s2;
       st.naccept[c] = nacc;
       st.nrej_win[c] = nrej;
       st.nevals[c] = nev;
       if (c == 0) *st.step = s_end;  // k_adapt reads the row it follows
     }
   }
-  if (w == kS2Wave && lane == 0) {
-    st.s2sum[c] = s2a.sum;
-    st.sq_mean[c] = s2a.qmean;
-    st.sq_m2[c] = s2a.qm2;
+  if (w == kSigWave) {
+    const double x0 = (p.updatesigma && gpend) ? 1.0 / (Gl * (2.0 / ss)) : s2c;
+    flush_s2(x0);
+    if (lane == 0) {
+      st.sigma2[c] = x0;
+      st.s2sum[c] = s2a.sum;
+      st.sq_mean[c] = s2a.qmean;
+      st.sq_m2[c] = s2a.qm2;
+    }
   }
 }
 
@@ -1285,7 +1346,8 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
     double r1, pr1, r2 = INFINITY, pr2 = 0.0;
     const bool inb1 = evaluate(u, 1.0, r1, pr1);
     // a12 (k_chain lane 0): ssA = r1 (+Inf out of bounds), prA = pr1 (0 out of bounds)
-    const double a12 = fmin(1.0, exp(-0.5 * (r1 - ss) / s2 - 0.5 * (pr1 - prior)));
+    const double ip = 1.0 / s2;  // k_chain's xip
+    const double a12 = fmin(1.0, exp(dram_log_ratio(r1, ss, pr1, prior, ip)));
     bool acc = false, acc2 = false;
     if (inb1) {
       nev += 1;
@@ -1296,11 +1358,10 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
       const bool inb2 = evaluate(u, inv_ds, r2, pr2);
       if (inb2) {
         nev += 1;
-        // a32 (lane 1), l2 (lane 2), a13 (level 3) as k_chain computes them
-        const double a32 = fmin(1.0, exp(-0.5 * (r1 - r2) / s2 - 0.5 * (pr1 - pr2)));
-        const double l2 = exp(-0.5 * (r2 - ss) / s2 - 0.5 * (pr2 - prior));
-        const double a13 = l2 * q1 * (1.0 - a32) / (1.0 - a12);
-        acc2 = U2 < a13;
+        // a32 (lane 1), l2 (lane 2) and the stage-2 test as k_chain computes them
+        const double a32 = fmin(1.0, exp(dram_log_ratio(r1, r2, pr1, pr2, ip)));
+        const double l2 = exp(dram_log_ratio(r2, ss, pr2, prior, ip));
+        acc2 = dram_dr_accept(U2, a12, a32, l2, q1);
       }
     }
     if (acc || acc2) {  // the accepted proposal is the last one evaluated: it is in yb
