@@ -36,7 +36,8 @@ extern "C" {
 #define TCI_ERANGE (-5)  /* cell id out of range, or ld_theta < 7 + N of that cell */
 
 #define TCI_MAX_SEG 4    /* stem-loop segments per dye (GetFluorFromPolPos.m:47 loop) */
-#define TCI_MAX_POINTS 513 /* acquisition points per cell supported by the kernels */
+#define TCI_MAX_POINTS 2048 /* acquisition points per cell: <= 513 run the register-resident kernels,
+                               longer cells the long-cell kernel (its tables in LDS, 64 B per point) */
 
 typedef struct tci_ctx tci_ctx;
 
@@ -68,7 +69,7 @@ typedef struct {
 
 typedef struct {
   int32_t device;
-  int32_t rows_per_lane;   /* kernel variant selected from the longest cell */
+  int32_t rows_per_lane;   /* kernel variant selected from the longest cell (0: the long-cell kernel) */
   int64_t n_cells;
   int64_t max_points;
   int64_t device_bytes;    /* resident cell-table bytes in HBM */

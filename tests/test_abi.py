@@ -90,7 +90,8 @@ def test_create_rejects_bad_input_before_touching_a_device(lib):
     assert rc == _lib.TCI_EINVAL and "increasing" in msg
     rc, msg = create([0.0, np.nan], [0, 2])
     assert rc == _lib.TCI_EINVAL
-    rc, msg = create(np.arange(600.0), [0, 600])
+    n = _lib.TCI_MAX_POINTS + 1  # past the long-cell kernel's LDS tables
+    rc, msg = create(np.arange(float(n)), [0, n])
     assert rc == _lib.TCI_EINVAL and "max" in msg
 
 

@@ -520,3 +520,40 @@ def test_engines_agree_on_the_two_segment_construct():
         for f in ("chain", "s2chain", "mean", "std", "final_theta", "accept_rate", "n_evals"):
             np.testing.assert_array_equal(getattr(out[eng], f), getattr(out["batched"], f), err_msg=f"{eng} {f}")
     assert np.median(out["walk"].accept_rate) > 0.01
+
+
+@pytest.mark.parametrize("n", [293, 600])
+def test_very_long_cells_sample_and_adapt(n):
+    """Cells past the fused engine's LDS budget (P = 300: the batched engine; N = 600: the
+    long-cell likelihood kernel too, R read from global memory in the proposal products and the
+    generic adaptation): the chains stay in bounds, are deterministic per seed, and the adapted
+    proposal is the scaled chain covariance (ConstantElongationSim.m:39-50 has no length cap)."""
+    from transcriptioncycleinference_amd import Likelihood, from_lists
+    from transcriptioncycleinference_amd.mcmc import DramOptions, dram_run
+
+    rng = np.random.default_rng(n)
+    cl = []
+    for _ in range(3):
+        t = 0.2454 * np.arange(n) + rng.uniform(-0.012, 0.012, n)
+        ms2 = rng.normal(20.0, 5.0, n)
+        pp7 = rng.normal(10.0, 3.0, n)
+        ms2[rng.random(n) < 0.37] = np.nan
+        cl.append((t, ms2, pp7))
+    with Likelihood(from_lists(cl), "P2P-MS2v5-LacZ-PP7v4", device=0) as L:
+        assert L.info["rows_per_lane"] == (8 if n <= 513 else 0)
+        ids = [0, 1, 2]
+        o = DramOptions(n_steps=300, burnintime=100, adaptint=100, stats_from=1, thin=1, seed=9)
+        x0, lo, hi, mu, sg, J0 = setup_rows(L.cells, ids, 0)
+        res = dram_run(L, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, want_qcov=True)
+        res2 = dram_run(L, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, want_qcov=True)
+    np.testing.assert_array_equal(res.chain, res2.chain)
+    P = 7 + n
+    for k in range(3):
+        X = res.chain[:300, k, :P]
+        assert np.all(X >= lo[k, :P]) and np.all(X <= hi[k, :P])
+        assert len(np.unique(X[:, 0])) > 5  # the chain moves
+        C = np.cov(X.T, ddof=1) + 1e-5 * np.eye(P)
+        R = res.qcov_R[k, :P, :P]
+        assert np.all(np.tril(R, -1) == 0)
+        want = (2.4 ** 2 / P) * C
+        np.testing.assert_allclose(R.T @ R, want, rtol=1e-6, atol=1e-6 * np.abs(want).max())

@@ -413,3 +413,90 @@ def test_synthetic_config4_cells(construct, c_oracle):
     assert rel_err(ss, want) <= REL
     # at the ground truth the residual is pure noise: SS ~ (0.63N)(1 + 4)
     assert 0.5 < np.median(ss) / (0.63 * 200 * 5) < 1.5
+
+
+# --- long cells (N > 513): the long-cell kernel (rows_per_lane == 0) -------------------
+
+
+def _long_cells(rng, n, ncell=3):
+    from transcriptioncycleinference_amd import from_lists
+    from transcriptioncycleinference_amd.data import synthetic_times
+
+    cl = []
+    for k in range(ncell):
+        nk = n - 7 * k  # ragged lengths in one context
+        t = synthetic_times(rng, nk)
+        y1, y2 = rng.normal(3, 2, nk), rng.normal(6, 3, nk)
+        y1[rng.random(nk) < 0.37] = np.nan
+        y2[rng.random(nk) < 0.37] = np.nan
+        cl.append((t, y1, y2))
+    return from_lists(cl)
+
+
+@pytest.mark.parametrize("n", [514, 600, 1000, 2048])
+def test_long_cells_vs_oracle(n, construct, c_oracle):
+    """ConstantElongationSim.m:39-50 has no length cap: cells past the register-resident variants
+    (N > 513) run the long-cell kernel, ss_batch and both forward grids against the oracle."""
+    from transcriptioncycleinference_amd import Likelihood
+    from transcriptioncycleinference_amd.data import draw_x0
+
+    rng = np.random.default_rng(300 + n)
+    cells = _long_cells(rng, n)
+    rows, cid = [], []
+    for k in range(24):
+        c = k % 3
+        r = draw_x0(rng, int(cells.lengths[c]))
+        if k % 4 == 0:
+            r[0] = rng.uniform(0.05, 0.5)  # slow elongation: long windows
+        rows.append(r)
+        cid.append(c)
+    theta = pack(rows)
+    cid = np.array(cid, np.int32)
+    active = np.ones(len(cid), np.uint8)
+    active[5] = 0
+    with Likelihood(cells, "P2P-MS2v5-LacZ-PP7v4") as L:
+        assert L.info["rows_per_lane"] == 0
+        ss = L.ss_batch(theta, cid, active)
+        fi = L.forward(theta[:3], cid[:3], grid="interp")
+        fr = L.forward(theta[:3], cid[:3], grid="raw")
+        L.set_force_exact(scan=True, positions=True)
+        ss_exact = L.ss_batch(theta, cid, active)
+        L.set_force_exact()
+    want = oracle_ss(c_oracle, cells, construct, theta, cid, active)
+    assert np.isinf(ss[5]) and np.isinf(want[5])
+    e, ex = rel_err(ss, want), rel_err(ss_exact, want)
+    print(f"N={n}: max rel err {e:.3e} (forced exact paths {ex:.3e})")
+    assert e <= REL and ex <= REL
+    for i in range(3):
+        t = cells.cell(int(cid[i]))[0]
+        nk = len(t)
+        for mode, (ms2, pp7) in ((1, fi), (0, fr)):
+            m, p = c_oracle.forward(t, construct, theta[i], mode=mode)
+            assert rel_err(ms2[i, :nk], m) <= 1e-12 and rel_err(pp7[i, :nk], p) <= 1e-12
+
+
+def test_long_cells_multi_segment_and_edges(c_oracle):
+    """Long cells on the 2-segment 3x-length construct (config 5) and the edge rows: non-finite
+    theta -> NaN, bad cell id rejected, all-NaN data -> 0."""
+    from transcriptioncycleinference_amd import Likelihood, from_lists, long_two_loop_construct
+    from transcriptioncycleinference_amd.data import draw_x0, synthetic_times
+
+    rng = np.random.default_rng(77)
+    n = 700
+    t = synthetic_times(rng, n)
+    y1, y2 = rng.normal(3, 2, n), rng.normal(6, 3, n)
+    cells = from_lists([(t, y1, y2), (t, np.full(n, np.nan), np.full(n, np.nan))])
+    con = long_two_loop_construct()
+    rows = [draw_x0(rng, n) for _ in range(10)]
+    rows[3][9] = np.inf
+    theta = pack(rows)
+    cid = np.array([0] * 9 + [1], np.int32)
+    ocs = O.Construct(con.L0, con.ms2_start, con.ms2_end, con.ms2_loopn, con.pp7_start, con.pp7_end, con.pp7_loopn)
+    with Likelihood(cells, con) as L:
+        assert L.info["rows_per_lane"] == 0
+        ss = L.ss_batch(theta, cid)
+    want, _ = c_oracle.ss_batch(cells.offsets, cells.t, cells.ms2, cells.pp7, ocs, theta, cid)
+    assert np.isnan(ss[3])
+    ok = np.arange(10) != 3
+    assert rel_err(ss[ok], want[ok]) <= REL
+    assert ss[9] == 0.0

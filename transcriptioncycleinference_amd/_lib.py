@@ -18,7 +18,7 @@ TCI_ENOMEM = -3
 TCI_EDIM = -4
 TCI_ERANGE = -5
 TCI_MAX_SEG = 4
-TCI_MAX_POINTS = 513
+TCI_MAX_POINTS = 2048
 TCI_GRID_INTERP = 0
 TCI_GRID_RAW = 1
 

@@ -156,11 +156,12 @@ void fill_segments(KParams* kp, const tci_construct* cs) {
   kp->emax = emax;
 }
 
+// Rows per lane of the register-resident kernel, or 0 for the long-cell kernel (N > 513).
 int pick_rpl(int64_t max_points) {
   const int64_t steps = max_points - 1;
   for (int r : {1, 2, 4, 8})
     if (64 * r >= steps) return r;
-  return -1;
+  return 0;
 }
 
 int run(tci_ctx* ctx, int mode, const double* theta, int64_t ld, const int32_t* cell, const uint8_t* active,
@@ -249,7 +250,8 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
     ctx->max_points = std::max(ctx->max_points, n);
   }
   ctx->rpl = pick_rpl(ctx->max_points);
-  const int64_t stride = 64 * (ctx->rpl + 1);  // records per cell: every slot/point index a wave touches
+  // records per cell: every slot/point index a wave touches (the long-cell kernel reads < N)
+  const int64_t stride = ctx->rpl > 0 ? 64 * (ctx->rpl + 1) : (ctx->max_points + 63) / 64 * 64;
   ctx->stride = stride;
   const size_t total = (size_t)C * (size_t)stride;
   std::vector<tci::StepRec> steps(total, tci::StepRec{0.0, 0.0}), steps_raw(total, tci::StepRec{0.0, 0.0});
@@ -329,6 +331,7 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
   if (!kp.cells || !kp.steps || !kp.steps_raw || !kp.points)
     return bail(fail(ctx, TCI_EHIP, "hipMemcpy(cell table) failed"));
   kp.cell_stride = stride;
+  kp.max_n = ctx->max_points;
   kp.n_cells = C;
   kp.force_exact = 0;
   fill_segments(&kp, construct);
@@ -664,7 +667,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   // chains x 200 points, 39 per CU) its chain walk + draws pass take 209 us per step against 1950 us
   // for the batched engine's per-step kernels, which stage every chain's R once per stage.
   const int64_t fused_lds = tci::dram_chain_lds_bytes(ld, ctx->rpl);
-  const bool fused_fits = fused_lds <= 160 * 1024;
+  const bool fused_fits = ctx->rpl > 0 && fused_lds <= 160 * 1024;  // long cells: the batched engine
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   // WALK (one wavefront per chain) once k_chain's one-workgroup-per-chain layout would need more

@@ -262,15 +262,16 @@ __device__ void load_R_f32(float* Rl, const DramState& st, int64_t c, int P) {
 // instance (the batched engine's 1-row proposals, the fused engine's 32-row draws) gives the same
 // bits.
 typedef double f64x4 __attribute__((ext_vector_type(4)));
+// top: the highest column tile of this call (tiles top, top-1, .. top+1-NWV*CT are computed):
+// (P + 15)/16 - 1 for one call; wider rows loop over tops (propose_block).
 template <int MT, int CT, int NWV, class Store>  // NWV: waves sharing the column tiles
-__device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const float* Rl, int P, Store store) {
+__device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const float* Rl, int P, int top, Store store) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int row = lane & 15, kq = lane >> 4;
-  const int ntiles = (P + 15) >> 4;
   int nt[CT], kmx[CT];
 #pragma unroll
   for (int g = 0; g < CT; ++g) {
-    nt[g] = ntiles - 1 - (NWV * g + ((g & 1) ? NWV - 1 - w : w));  // uniform: costliest first, snake order
+    nt[g] = top - (NWV * g + ((g & 1) ? NWV - 1 - w : w));  // uniform: costliest first, snake order
     kmx[g] = nt[g] >= 0 ? min(16 * nt[g] + 15, P - 1) : -1;
   }
   // The tiles are in decreasing k-extent (kmx[0] >= kmx[1] >= ..), so the k-steps split into
@@ -319,7 +320,7 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
       }
   }
 }
-constexpr int kZrCT = 5;  // column tiles per wave: P <= 320 (the per-stage kernels' LDS allows P <= 281)
+constexpr int kZrCT = 5;  // column tiles per wave and call: 20 per 4-wave call (P <= 320 in one call)
 
 // Dynamic LDS of the per-stage kernels (vector stride L = ld >= P): z, y, red and the chain's R
 // as packed fp32.
@@ -330,7 +331,12 @@ struct Smem {
   float* Rl;
   int L;
 };
-__host__ __device__ inline int64_t stage_lds_bytes(int64_t L) { return (2 * L + 8) * 8 + (L * (L + 1) / 2) * 4 + 16; }
+// R is staged into LDS only while it fits (stage_r_lds); longer rows read the packed fp32 R from
+// global memory in the same MFMA order (the same bits).
+__host__ __device__ inline bool stage_r_lds(int64_t L) { return (2 * L + 8) * 8 + (L * (L + 1) / 2) * 4 + 16 <= 150 * 1024; }
+__host__ __device__ inline int64_t stage_lds_bytes(int64_t L) {
+  return (2 * L + 8) * 8 + (stage_r_lds(L) ? (L * (L + 1) / 2) * 4 : 0) + 16;
+}
 __device__ __forceinline__ Smem stage_smem(double* dyn, int L) {
   Smem m;
   m.z = dyn;
@@ -371,11 +377,14 @@ __device__ bool propose_block(const DramState& st, const DramParams& p, int64_t 
                               const double* base, double scale, int P, double* out, Smem& sm) {
   const int64_t ld = st.ld;
   draw_normals(p.seed, st.key[c], step, purpose, P, sm.z, threadIdx.x);
-  load_R_f32(sm.Rl, st, c, P);
+  const bool rl = stage_r_lds(st.ld);
+  if (rl) load_R_f32(sm.Rl, st, c, P);
   __syncthreads();
   double* U = sm.y;
   const int us = sm.L;
-  mfma_zr<1, kZrCT, 4>(sm.z, sm.L, 1, sm.Rl, P, [=](int r, int j, double v) { U[r * us + j] = v; });
+  const float* Rsrc = rl ? sm.Rl : st.Rf + c * tri_stride(st.ld);
+  for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= 4 * kZrCT)
+    mfma_zr<1, kZrCT, 4>(sm.z, sm.L, 1, Rsrc, P, top, [=](int r, int j, double v) { U[r * us + j] = v; });
   __syncthreads();
   int inb = 1;
   for (int j = threadIdx.x; j < P; j += kThreads) {
@@ -786,7 +795,7 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
     // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
     double* d0 = drow + step0 * DW;
     if (!(TCI_DRAWS_ABLATE & 2))
-      mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rl, P,
+      mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rl, P, ((P + 15) >> 4) - 1,
                               [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; });
     for (int k = w; k < ns; k += kDrawWaves) {
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
@@ -1436,241 +1445,9 @@ int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, 
 }
 
 
-// Adaptation for chains whose packed covariance fits in LDS (P(P+1)/2 doubles: P <= 139 keeps two
-// workgroups per CU). Thread t owns the 4x4 tiles t, t + 256, .. (row-major over the upper
-// triangle of the tile grid) in registers.
-//   covupd: the window's rows (staged through LDS in batches) give the batch mean and scatter
-//     sum_r (x_r - m)'(x_r - m) (16 FMAs per tile and row), merged into (cov, mean, wsum) by the
-//     pairwise-update formula -- the same numbers as mcmcstat's row-by-row recurrence in exact
-//     arithmetic, with 2 barriers per batch instead of 2 per row.
-//   Cholesky of cov + qcovadj I: blocked LDL' with 4-column panels: a tile row is stored to the
-//     packed LDS triangle when it becomes the panel, wave 0 eliminates inside the panel, every
-//     owner applies the rank-4 update to its later tiles in registers (2 barriers per panel).
-//     R rows are the panel rows scaled by adascale / sqrt(pivot).
 #ifndef TCI_ADAPT_ABLATE
 #define TCI_ADAPT_ABLATE 0  // diagnostics only (wrong results): bit0 skip the Cholesky, bit1 skip the covupd passes
 #endif
-constexpr int kAdaptTiles = 3;  // tiles per thread: NT(NT+1)/2 <= 768, NT = ceil(P/4)
-__host__ __device__ inline int adapt_ls(int P) { return (P + 3) & ~3; }
-__host__ __device__ inline int64_t adapt_tiles_lds_bytes(int64_t P) {
-  const int64_t tri = P * (P + 1) / 2, Ls = (P + 3) & ~3;
-  return (tri + 2 * Ls + 8) * 8;
-}
-
-__global__ __launch_bounds__(kThreads) void k_adapt_tiles(DramState st, DramParams p) {
-  extern __shared__ __attribute__((aligned(16))) double dyn[];
-  __shared__ int fail;
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int64_t c = blockIdx.x;
-  const int64_t step = *st.step;
-  if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
-  const int64_t ld = st.ld;
-  const int P = st.npar[c];
-  const int NT = (P + 3) >> 2, Ls = adapt_ls(P);
-  const int tri = P * (P + 1) / 2;
-  double* A = dyn;         // phase 1-2: window batches [rb][Ls]; phase 4: packed upper triangle
-  double* mb = A + tri;    // batch mean (Ls)
-  double* mo = mb + Ls;    // old mean (Ls)
-  double* cvg = st.cov + c * ld * ld;
-  double* mu = st.cmean + c * ld;
-  double* R = st.R + c * ld * ld;
-  auto off = [P](int i) { return i * P - (i * (i - 1)) / 2; };
-  // ---- owned tiles (ti, tj), ti <= tj, by walking the row-major tile order from t
-  int ti_[kAdaptTiles], tj_[kAdaptTiles];
-  {
-    int ti = 0, tj = t;
-    while (ti < NT && tj >= NT) {
-      tj = tj - NT + ti + 1;
-      ++ti;
-    }
-#pragma unroll
-    for (int k = 0; k < kAdaptTiles; ++k) {
-      ti_[k] = ti < NT ? ti : -1;
-      tj_[k] = tj;
-      tj += kThreads;
-      while (ti < NT && tj >= NT) {
-        tj = tj - NT + ti + 1;
-        ++ti;
-      }
-    }
-  }
-  const int nb = (TCI_ADAPT_ABLATE & 2) ? 0 : (int)p.adaptint;
-  const int rb = max(1, min((int)p.adaptint, tri / Ls));  // rows per LDS batch
-  const double* win = st.window + c * p.adaptint * ld;
-  // ---- pass 1: batch mean (row order fixed: deterministic)
-  double s0 = 0.0, s1 = 0.0;
-  for (int r0 = 0; r0 < nb; r0 += rb) {
-    const int n = min(rb, nb - r0);
-    for (int e = t; e < n * Ls; e += kThreads) {
-      const int r = e / Ls, j = e - r * Ls;
-      A[e] = j < P ? win[(int64_t)(r0 + r) * ld + j] : 0.0;
-    }
-    __syncthreads();
-    for (int r = 0; r < n; ++r) {
-      if (t < Ls) s0 += A[r * Ls + t];
-      if (t + kThreads < Ls) s1 += A[r * Ls + t + kThreads];
-    }
-    __syncthreads();
-  }
-  if (t < Ls) {
-    mb[t] = t < P ? s0 / (double)nb : 0.0;
-    mo[t] = t < P ? mu[t] : 0.0;
-  }
-  if (t + kThreads < Ls) {
-    mb[t + kThreads] = t + kThreads < P ? s1 / (double)nb : 0.0;
-    mo[t + kThreads] = t + kThreads < P ? mu[t + kThreads] : 0.0;
-  }
-  __syncthreads();
-  // ---- pass 2: scatter of the deviations from the batch mean, per owned tile
-  double acc[kAdaptTiles][16];
-  double mi[kAdaptTiles][4], mj[kAdaptTiles][4];
-#pragma unroll
-  for (int k = 0; k < kAdaptTiles; ++k) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[k][q] = 0.0;
-    const int ti = max(ti_[k], 0), tj = ti_[k] >= 0 ? tj_[k] : 0;
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      mi[k][a] = mb[4 * ti + a];
-      mj[k][a] = mb[4 * tj + a];
-    }
-  }
-  for (int r0 = 0; r0 < nb; r0 += rb) {
-    const int n = min(rb, nb - r0);
-    for (int e = t; e < n * Ls; e += kThreads) {
-      const int r = e / Ls, j = e - r * Ls;
-      A[e] = j < P ? win[(int64_t)(r0 + r) * ld + j] : 0.0;
-    }
-    __syncthreads();
-    for (int r = 0; r < n; ++r) {
-      const double* x = A + r * Ls;
-#pragma unroll
-      for (int k = 0; k < kAdaptTiles; ++k) {
-        if (ti_[k] < 0) continue;
-        const double2* xi = reinterpret_cast<const double2*>(x + 4 * ti_[k]);
-        const double2* xj = reinterpret_cast<const double2*>(x + 4 * tj_[k]);
-        const double2 i01 = xi[0], i23 = xi[1], j01 = xj[0], j23 = xj[1];
-        const double di[4] = {i01.x - mi[k][0], i01.y - mi[k][1], i23.x - mi[k][2], i23.y - mi[k][3]};
-        const double dj[4] = {j01.x - mj[k][0], j01.y - mj[k][1], j23.x - mj[k][2], j23.y - mj[k][3]};
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) acc[k][4 * a + b] = fma(di[a], dj[b], acc[k][4 * a + b]);
-      }
-    }
-    __syncthreads();
-  }
-  // ---- merge (cov, mean, wsum) with the batch: n = na + nb, d = m_batch - m_old
-  const double na = st.wsum[c], n = na + (double)nb;
-  const double fcross = na * (double)nb / n;
-#pragma unroll
-  for (int k = 0; k < kAdaptTiles; ++k) {
-    if (ti_[k] < 0) continue;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int i = 4 * ti_[k] + a, j = 4 * tj_[k] + b;
-        if (i >= P || j >= P || j < i) continue;
-        double cv;
-        if (n <= 1.0) {
-          cv = 0.0;  // a single row so far: covariance 0 (the recurrence's first row)
-        } else if (na == 0.0) {
-          cv = acc[k][4 * a + b] / (n - 1.0);
-        } else {
-          const double di = mb[i] - mo[i], dj = mb[j] - mo[j];
-          cv = (cvg[(int64_t)i * ld + j] * (na - 1.0) + acc[k][4 * a + b] + di * dj * fcross) / (n - 1.0);
-        }
-        cvg[(int64_t)i * ld + j] = cv;
-        acc[k][4 * a + b] = cv + (i == j ? p.qcovadj : 0.0);  // the matrix the Cholesky factors
-      }
-  }
-  for (int j = t; j < P; j += kThreads) mu[j] = na == 0.0 ? mb[j] : mo[j] + (mb[j] - mo[j]) * ((double)nb / n);
-  if (t == 0) st.wsum[c] = n;
-  if (step < p.burnintime) {
-    // burn-in: no covariance adaptation, only scaling by the window's rejection rate
-    const double rate = (double)st.nrej_win[c] / (double)p.adaptint;
-    double s = 1.0;
-    if (rate > 0.95) s = 1.0 / p.burnin_scale;
-    else if (rate < 0.05) s = p.burnin_scale;
-    if (s != 1.0) {
-      for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
-        const int i = (int)(e / P), j = (int)(e % P);
-        store_R(st, c, P, i, j, f32_round(R[(int64_t)i * ld + j] * s));
-      }
-    }
-    __syncthreads();
-    if (t == 0) st.nrej_win[c] = 0;
-    return;
-  }
-  // ---- blocked LDL' of cov + qcovadj I on the packed triangle
-  if (t == 0) fail = 0;
-  __syncthreads();
-  for (int pp = 0; pp < ((TCI_ADAPT_ABLATE & 1) ? 0 : NT); ++pp) {
-#pragma unroll
-    for (int k = 0; k < kAdaptTiles; ++k) {
-      if (ti_[k] != pp) continue;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int i = 4 * pp + a, j = 4 * tj_[k] + b;
-          if (i < P && j < P && j >= i) A[off(i) + j - i] = acc[k][4 * a + b];
-        }
-    }
-    __syncthreads();
-    const int k0 = 4 * pp, k1 = min(4 * pp + 3, P - 1);
-    if (w == 0) {  // eliminate inside the panel rows
-      for (int k = k0; k <= k1; ++k) {
-        const int ok = off(k);
-        const double d = A[ok];
-        if (!(d > 0.0) || !isfinite(d)) {
-          if (lane == 0) fail = 1;
-          break;
-        }
-        for (int kp = k + 1; kp <= k1; ++kp) {
-          const double f = A[ok + kp - k] / d;
-          const int okp = off(kp);
-          for (int j = kp + lane; j < P; j += 64) A[okp + j - kp] -= f * A[ok + j - k];
-        }
-        wave_sync();
-      }
-    }
-    __syncthreads();
-    if (fail) break;
-    // rank-4 update of every owned later tile: A[i][j] -= A[k][i] * A[k][j] / A[k][k]
-#pragma unroll
-    for (int k = 0; k < kAdaptTiles; ++k) {
-      if (ti_[k] <= pp) continue;
-      for (int kk = k0; kk <= k1; ++kk) {
-        const int ok = off(kk);
-        const double inv = 1.0 / A[ok];
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          const int i = 4 * ti_[k] + a;
-          const double sa = (i < P ? A[ok + i - kk] : 0.0) * inv;
-#pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const int j = 4 * tj_[k] + b;
-            acc[k][4 * a + b] -= sa * (j < P ? A[ok + j - kk] : 0.0);
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (!fail && !(TCI_ADAPT_ABLATE & 1)) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
-    const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
-    for (int i = 0; i < P; ++i) {
-      const int oi = off(i);
-      const double di = sqrt(A[oi]);
-      for (int j = i + t; j < P; j += kThreads) store_R(st, c, P, i, j, f32_round(A[oi + j - i] / di * sc));
-    }
-  }
-  __syncthreads();
-  if (t == 0) st.nrej_win[c] = 0;
-}
 
 // Lane (16 g + K)'s x in every lane of 16-lane row g (DPP row_newbcast, no LDS).
 template <int K>
@@ -2061,15 +1838,6 @@ int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
 #else
   if (p.pmax <= 16 * 13) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
 #endif
-  const int64_t ntile = (p.pmax + 3) / 4;
-  if (ntile * (ntile + 1) / 2 <= (int64_t)kAdaptTiles * kThreads && adapt_tiles_lds_bytes(p.pmax) <= 78 * 1024) {
-    const size_t bytes = (size_t)adapt_tiles_lds_bytes(p.pmax);
-    if (bytes > 48 * 1024 && hipFuncSetAttribute((const void*)k_adapt_tiles, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)bytes) != hipSuccess)
-      return TCI_EHIP;
-    hipLaunchKernelGGL(k_adapt_tiles, chain_grid(st.n_chains), dim3(kThreads), bytes, (hipStream_t)stream, st, p);
-    return finish();
-  }
   const size_t lds = p.lds_matrix ? (size_t)p.lds_matrix : 0;
   if (lds > 0 && hipFuncSetAttribute((const void*)k_adapt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
                      hipSuccess)

@@ -141,27 +141,30 @@ struct Regions {
 //   J_i = sum_{i' <= i} i' * c_i'
 // Both are integers < 2^53, exact in any summation order. KJ points at i = 0 of a table whose
 // SLOTS+RPL entries below i = 0 are zeros, so every index r - m - 1 >= -SLOTS needs no clamp.
-__device__ __forceinline__ double2 kj_at(const double2* KJ, int i) { return KJ[i]; }
+// CLAMP (the long-cell kernel): the table has ONE zero entry below i = 0 and lower indices read it.
+template <bool CLAMP = false>
+__device__ __forceinline__ double2 kj_at(const double2* KJ, int i) { return KJ[CLAMP ? max(i, -1) : i]; }
 
 // Row sum of one segment of one dye on the fast path (see the header), O(1) per row:
 //   full  (e < P_m < L, m in [f_lo, f_hi]):  phi * (K[r - f_lo] - K[r - f_hi - 1])
 //   ramp  (a < P_m < e, m in [r_lo, r_hi]):  sum_m c_{r-m} * (m*vd0 - a) * k
 //        = (k*vd0) * sum_m m*c_{r-m}  -  (k*a) * sum_m c_{r-m},   sum_m m*c_{r-m} = r*C - (J_hi - J_lo)
 // kvd = k*vd0 and ka = k*a are wave constants; C, J differences and r*C - dJ are exact integers.
+template <bool CLAMP = false>
 __device__ __forceinline__ double row_sum(const double2* KJ, int r, double rd, const Regions& rg,
                                           const SegParams& s, double kvd, double ka) {
   double acc = 0.0;
-  if (rg.f_lo <= rg.f_hi) acc = s.phi * (kj_at(KJ, r - rg.f_lo).x - kj_at(KJ, r - rg.f_hi - 1).x);
+  if (rg.f_lo <= rg.f_hi) acc = s.phi * (kj_at<CLAMP>(KJ, r - rg.f_lo).x - kj_at<CLAMP>(KJ, r - rg.f_hi - 1).x);
   if (rg.r_lo <= rg.r_hi) {
 #if TCI_RAMP_PREFIX
-    const double2 hi = kj_at(KJ, r - rg.r_lo), lo = kj_at(KJ, r - rg.r_hi - 1);
+    const double2 hi = kj_at<CLAMP>(KJ, r - rg.r_lo), lo = kj_at<CLAMP>(KJ, r - rg.r_hi - 1);
     const double C = hi.x - lo.x;
     const double Mc = fma(rd, C, -(hi.y - lo.y));  // sum of m * c_{r-m}, exact
     acc = fma(kvd, Mc, fma(-ka, C, acc));
 #else
-    double kA = kj_at(KJ, r - rg.r_lo).x;
+    double kA = kj_at<CLAMP>(KJ, r - rg.r_lo).x;
     for (int m = rg.r_lo; m <= rg.r_hi; ++m) {
-      const double kB = kj_at(KJ, r - m - 1).x;
+      const double kB = kj_at<CLAMP>(KJ, r - m - 1).x;
       acc = fma(kA - kB, fma((double)m, kvd, -ka), acc);
       kA = kB;
     }

@@ -50,7 +50,9 @@ struct KParams {
   const StepRec* steps_raw;  // raw times t and raw steps (forward on raw t, TranscriptionCycleMCMC.m:307)
   const PointRec* points;
   int64_t n_cells;
-  int64_t cell_stride;       // records per cell in steps/steps_raw/points (= 64*(rows_per_lane+1))
+  int64_t cell_stride;       // records per cell in steps/steps_raw/points (64*(rows_per_lane+1); long cells: N_max
+                             // rounded up to 64)
+  int64_t max_n;             // longest cell (points): sizes the long-cell kernel's LDS
   double L0;            // gene length before tau*v (GetFluorFromPolPos.m:19)
   double emax;          // max loop end over all segments and dyes
   int32_t n_seg;
@@ -62,7 +64,8 @@ struct KParams {
 
 enum Mode : int { MODE_SS = 0, MODE_FWD_INTERP = 1, MODE_FWD_RAW = 2 };
 
-// Launch the batched kernel (device pointers). rpl = rows per lane (1,2,4,8).
+// Launch the batched kernel (device pointers). rpl = rows per lane (1,2,4,8); 0 = the long-cell
+// kernel (tci_tile_kernel, any N up to TCI_MAX_POINTS).
 // out0/out1: MODE_SS -> out0 = ss[B]; forward modes -> MS2/PP7 rows of ld_out.
 int launch(const KParams& kp, int rpl, int mode, const double* theta, int64_t ld_theta,
            const int32_t* cell_id, const uint8_t* active, int64_t B, double* out0, double* out1,
