@@ -226,7 +226,7 @@ def end_to_end(lk, n_steps: int, seed: int, reduce=None):
             "accept_rate_median_rank0": float(np.median(fr.accept_rate))}
 
 
-def synthetic_config_cells(cfg: int, rank: int, world: int, device_index: int):
+def synthetic_config_cells(cfg: int, rank: int, world: int, device_index: int, n_points: int = 200):
     """this rank's shard of the 10,000 synthetic cells x 200 points
     (data seed 20201028 + rank) and the construct (config 5: 2 segments per dye, 3x length)."""
     from transcriptioncycleinference_amd import Likelihood, from_lists
@@ -234,7 +234,7 @@ def synthetic_config_cells(cfg: int, rank: int, world: int, device_index: int):
     from transcriptioncycleinference_amd.data import synthetic_cells
 
     construct = builtin_construct(CONSTRUCT) if cfg == 4 else long_two_loop_construct()
-    n_total, n_points = 10000, 200
+    n_total = 10000
     lo, hi = rank * n_total // world, (rank + 1) * n_total // world
 
     def fwd(times, theta):
@@ -302,7 +302,7 @@ def synthetic_kernel(cfg: int, rank: int, world: int, device_index: int, proposa
 
 
 def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_steps: int, reduce,
-                         engine: str = "auto"):
+                         engine: str = "auto", n_points: int = 200):
     """SURVEY.md §8(d) configs 4/5 end to end: this rank's shard of the 10,000 synthetic cells
     fitted by the GPU-resident DRAM (one chain per cell, n_burn = n_steps/20), as
     `parallel.fit_sharded` runs it minus the results gather. Strong scaling: 10,000 cells in total.
@@ -310,7 +310,7 @@ def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_s
     from transcriptioncycleinference_amd import Likelihood
     from transcriptioncycleinference_amd.mcmc import DramOptions, fit
 
-    cells, _, construct, n_total, n_points, lo, hi = synthetic_config_cells(cfg, rank, world, device_index)
+    cells, _, construct, n_total, n_points, lo, hi = synthetic_config_cells(cfg, rank, world, device_index, n_points)
     with Likelihood(cells, construct, device=device_index) as lk:
         reduce(0.0, "max")  # barrier
         t0 = time.perf_counter()

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Time the GPU-resident DRAM fit of BASELINE configs 4/5 (10,000 synthetic cells x 200 points) on
-one GPU:  python scripts/synth_dram_time.py CFG STEPS [CFG STEPS ...]   (TCI_ENGINE=auto|fused|batched|walk, TCI_LIB=variant .so)"""
+one GPU:  python scripts/synth_dram_time.py CFG STEPS [CFG STEPS ...]   (TCI_ENGINE=auto|fused|batched|walk, TCI_LIB=variant .so,
+TCI_SYNTH_POINTS=points per cell, default 200)"""
 import json
 import os
 import sys
@@ -18,4 +19,5 @@ args = sys.argv[1:]
 for i in range(0, len(args), 2):
     cfg, steps = int(args[i]), int(args[i + 1])
     print(json.dumps(bench.synthetic_end_to_end(cfg, 0, 1, 0, steps, reduce=lambda x, op: x,
-                                                    engine=os.environ.get("TCI_ENGINE", "auto"))), flush=True)
+                                                    engine=os.environ.get("TCI_ENGINE", "auto"),
+                                                    n_points=int(os.environ.get("TCI_SYNTH_POINTS", "200")))), flush=True)

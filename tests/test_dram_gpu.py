@@ -546,7 +546,15 @@ def test_very_long_cells_sample_and_adapt(n):
         x0, lo, hi, mu, sg, J0 = setup_rows(L.cells, ids, 0)
         res = dram_run(L, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, want_qcov=True)
         res2 = dram_run(L, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, want_qcov=True)
+        others = {}
+        if n <= 513:  # the fused and walk engines (R read from global memory in the draws pass)
+            for eng in ("batched", "fused", "walk"):
+                o.engine = eng
+                others[eng] = dram_run(L, np.array(ids, np.int32), x0, lo, hi, mu, sg, J0, 1.0, o, want_qcov=True)
     np.testing.assert_array_equal(res.chain, res2.chain)
+    for eng, r in others.items():
+        np.testing.assert_array_equal(r.chain, res.chain, err_msg=eng)
+        np.testing.assert_array_equal(r.qcov_R, res.qcov_R, err_msg=eng)
     P = 7 + n
     for k in range(3):
         X = res.chain[:300, k, :P]

@@ -541,6 +541,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
       if (!(qcov_diag[c * L + j] > 0)) return fail(ctx, TCI_EINVAL, "tci_dram_run: qcov_diag must be > 0");
     }
   }
+  const int64_t p_max_all = *std::max_element(npar.begin(), npar.end());  // > 208: k_adapt_gt's tile grid
   TCI_HIP(ctx, hipSetDevice(ctx->device));
   DevAllocs A;
   hipError_t e = hipSuccess;
@@ -583,7 +584,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(R, double, n * L2);
   TCI_ALLOC(Rf, float, n * (L * (L + 1) / 2));
   TCI_ALLOC(cov, double, n * L2);
-  TCI_ALLOC(work, double, n * L2);
+  TCI_ALLOC(work, double, p_max_all > 208 ? n * (size_t)((L + 15) / 16 * 16) * ((L + 15) / 16 * 16) : 1);
   TCI_ALLOC(cmean, double, n * L);
   TCI_ALLOC(wsum, double, n);
   TCI_ALLOC(window, double, n * (size_t)win * L);
@@ -659,7 +660,6 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_HIP(ctx, hipEventRecord(ev0, s));
   int64_t p_max = 0;
   for (size_t c = 0; c < n; ++c) p_max = std::max<int64_t>(p_max, npar[c]);
-  p.lds_matrix = p_max * p_max * (int64_t)sizeof(double) <= 150 * 1024 ? p_max * p_max * (int64_t)sizeof(double) : 0;
   p.pmax = p_max;
   const int64_t ai = opt->adaptint;
   // the fused engine's draws pass keeps a chain's R (packed fp32) and a tile of normals and products

@@ -604,110 +604,6 @@ __global__ void k_step_incr(int64_t* step) {
   if (threadIdx.x == 0) *step += 1;
 }
 
-// Adaptation, one workgroup per chain (launched only at steps that are multiples of adaptint).
-// Matrices live in LDS when P*P*8 bytes fit (every TestData cell: P <= 136), else in global.
-__global__ __launch_bounds__(kThreads) void k_adapt(DramState st, DramParams p) {
-  extern __shared__ __attribute__((aligned(16))) double dyn[];
-  __shared__ double xs[kVec];
-  __shared__ double dm[kVec];
-  __shared__ int fail;
-  const int t = threadIdx.x;
-  const int64_t c = blockIdx.x;
-  const int64_t step = *st.step;
-  if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
-  const int64_t ld = st.ld;
-  const int P = st.npar[c];
-  double* cvg = st.cov + c * ld * ld;
-  double* mu = st.cmean + c * ld;
-  double* R = st.R + c * ld * ld;
-  const bool in_lds = p.lds_matrix != 0;
-  double* A = in_lds ? dyn : st.work + c * ld * ld;
-  const int64_t lda = in_lds ? P : ld;
-  // ---- covupd: fold the window rows (chain rows step-adaptint+1 .. step) into (mean, cov, wsum)
-  for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
-    const int i = (int)(e / P), j = (int)(e % P);
-    if (j >= i) A[(int64_t)i * lda + j] = cvg[(int64_t)i * ld + j];
-  }
-  double ws = st.wsum[c];
-  __syncthreads();
-  for (int64_t r = 0; r < p.adaptint; ++r) {
-    const double* x = st.window + (c * p.adaptint + r) * ld;
-    for (int j = t; j < P; j += kThreads) xs[j] = x[j];
-    __syncthreads();
-    if (ws == 0.0) {  // first row: mean = x, cov = 0
-      for (int j = t; j < P; j += kThreads) mu[j] = xs[j];
-      __syncthreads();
-      ws = 1.0;
-      continue;
-    }
-    for (int j = t; j < P; j += kThreads) dm[j] = xs[j] - mu[j];
-    __syncthreads();
-    // xcov = oldcov + w/(w+oldwsum-1) * (oldwsum/(w+oldwsum) * d'd - oldcov), w = 1
-    const double f1 = 1.0 / ws, f2 = ws / (ws + 1.0);
-    for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
-      const int i = (int)(e / P), j = (int)(e % P);
-      if (j < i) continue;
-      const double old = A[(int64_t)i * lda + j];
-      A[(int64_t)i * lda + j] = old + f1 * (f2 * dm[i] * dm[j] - old);
-    }
-    for (int j = t; j < P; j += kThreads) mu[j] = mu[j] + dm[j] / (ws + 1.0);
-    ws += 1.0;
-    __syncthreads();
-  }
-  for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
-    const int i = (int)(e / P), j = (int)(e % P);
-    if (j >= i) cvg[(int64_t)i * ld + j] = A[(int64_t)i * lda + j];
-  }
-  if (t == 0) st.wsum[c] = ws;
-  __syncthreads();  // the copy-back must read A before the Cholesky below modifies it
-  if (step < p.burnintime) {
-    // burn-in: no covariance adaptation, only scaling by the window's rejection rate
-    const double rate = (double)st.nrej_win[c] / (double)p.adaptint;
-    double s = 1.0;
-    if (rate > 0.95) s = 1.0 / p.burnin_scale;
-    else if (rate < 0.05) s = p.burnin_scale;
-    if (s != 1.0) {
-      for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
-        const int i = (int)(e / P), j = (int)(e % P);
-        store_R(st, c, P, i, j, f32_round(R[(int64_t)i * ld + j] * s));
-      }
-    }
-    __syncthreads();
-    if (t == 0) st.nrej_win[c] = 0;
-    return;
-  }
-  // ---- R = chol(cov + qcovadj*I) * adascale (upper, A = R'R), in place on A
-  for (int i = t; i < P; i += kThreads) A[(int64_t)i * lda + i] += p.qcovadj;
-  if (t == 0) fail = 0;
-  __syncthreads();
-  for (int k = 0; k < P; ++k) {
-    if (t == 0) {
-      const double d = A[(int64_t)k * lda + k];
-      if (!(d > 0.0) || !isfinite(d)) fail = 1;
-      A[(int64_t)k * lda + k] = sqrt(d);
-    }
-    __syncthreads();
-    if (fail) break;
-    const double dk = A[(int64_t)k * lda + k];
-    for (int j = k + 1 + t; j < P; j += kThreads) A[(int64_t)k * lda + j] /= dk;
-    __syncthreads();
-    const int m = P - k - 1;
-    for (int64_t e = t; e < (int64_t)m * m; e += kThreads) {
-      const int i = k + 1 + (int)(e / m), j = k + 1 + (int)(e % m);
-      if (j >= i) A[(int64_t)i * lda + j] -= A[(int64_t)k * lda + i] * A[(int64_t)k * lda + j];
-    }
-    __syncthreads();
-  }
-  if (!fail) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
-    const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
-    for (int64_t e = t; e < (int64_t)P * P; e += kThreads) {
-      const int i = (int)(e / P), j = (int)(e % P);
-      store_R(st, c, P, i, j, j >= i ? f32_round(A[(int64_t)i * lda + j] * sc) : 0.0);
-    }
-  }
-  __syncthreads();
-  if (t == 0) st.nrej_win[c] = 0;
-}
 
 
 // ---- Fused chain engine. Per chunk of chain rows between two adaptations (R fixed):
@@ -760,8 +656,13 @@ enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a d
 
 // Dynamic LDS of k_draws: one pass's normals (2 x kDrawSteps rows of stride L) and the chain's R
 // as packed fp32.
+// R is staged only while it fits beside the normals; longer rows read the packed fp32 R from global
+// memory in the same MFMA order (the same bits).
+__host__ __device__ inline bool draws_r_lds(int64_t L) {
+  return (2 * kDrawSteps * L) * 8 + (L * (L + 1) / 2) * 4 + 16 <= 160 * 1024;
+}
 __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
-  return (2 * kDrawSteps * L) * 8 + (L * (L + 1) / 2) * 4 + 16;
+  return (2 * kDrawSteps * L) * 8 + (draws_r_lds(L) ? (L * (L + 1) / 2) * 4 : 0) + 16;
 }
 
 // NWD waves per workgroup: 4 for the FUSED engine (299 TestData chains: 100.6 vs 105.4 ms per 20k
@@ -782,7 +683,9 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   double* Z = dyn;
   float* Rl = reinterpret_cast<float*>(Z + 2 * kDrawSteps * L);
-  if (!(TCI_DRAWS_ABLATE & 8)) load_R_f32<kDrawThreads>(Rl, st, c, P);
+  const bool rl = draws_r_lds(ld);
+  if (rl && !(TCI_DRAWS_ABLATE & 8)) load_R_f32<kDrawThreads>(Rl, st, c, P);
+  const float* Rsrc = rl ? Rl : st.Rf + c * tri_stride(ld);
   const double a = 0.5 * (double)st.nobs[c];
   const double inv_ds = 1.0 / p.drscale;
   double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
@@ -795,8 +698,9 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
     // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
     double* d0 = drow + step0 * DW;
     if (!(TCI_DRAWS_ABLATE & 2))
-      mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rl, P, ((P + 15) >> 4) - 1,
-                              [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; });
+      for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT)
+        mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rsrc, P, top,
+                                              [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; });
     for (int k = w; k < ns; k += kDrawWaves) {
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
       if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
@@ -1210,7 +1114,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       st.naccept[c] = nacc;
       st.nrej_win[c] = nrej;
       st.nevals[c] = nev;
-      if (c == 0) *st.step = s_end;  // k_adapt reads the row it follows
+      if (c == 0) *st.step = s_end;  // the adaptation reads the row it follows
     }
   }
   if (w == kSigWave) {
@@ -1409,7 +1313,7 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
     st.s2sum[c] = s2a.sum;
     st.sq_mean[c] = s2a.qmean;
     st.sq_m2[c] = s2a.qm2;
-    if (c == 0) *st.step = s_end;  // k_adapt reads the row it follows
+    if (c == 0) *st.step = s_end;  // the adaptation reads the row it follows
   }
 }
 
@@ -1783,6 +1687,242 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8
   if (t == 0) st.nrej_win[c] = 0;
 }
 
+// ---- Adaptation for P > 208 (past k_adapt_mfma's register-resident tiles): the same covupd merge
+// and right-looking blocked Cholesky by 16 x 16 tiles on the matrix cores, with the tiles in global
+// memory -- st.work as an NT x NT grid of 16 x 16 tiles per chain (tile (ti, tj) at (ti NT + tj) 256,
+// element (r, col) at r 16 + col), L2-resident while the chain's workgroup works on it. One
+// workgroup of kGtWaves waves per chain:
+//   covupd: passes of kGtTiles tiles per wave; each pass streams the window's centred rows through
+//     LDS in batches of rb rows (as many as fit 96 KB, a multiple of 4) and accumulates the owned
+//     tiles' scatter with v_mfma_f64_16x16x4_f64, then merges them into (cov, mean, wsum) with
+//     k_adapt_mfma's formula and writes cov + qcovadj I to the tile grid;
+//   Cholesky: per panel pk, wave 0 factors the diagonal tile in registers (chol16_step), 16-lane
+//     groups solve the panel's row tiles, every wave takes trailing tiles (pk < ti <= tj) round-robin
+//     and applies the rank-16 update as 4 MFMAs. R = U * adascale, stored only when every pivot
+//     was positive (a singular matrix keeps the previous R, as mcmcstat).
+// The tile arithmetic is k_adapt_mfma's, so both kernels give the same R up to the order of the
+// scatter's k-steps (rows in batches here).
+constexpr int kGtWaves = 8, kGtTiles = 8;
+__host__ __device__ inline int64_t gt_lt(int64_t ld) { return (ld + 15) / 16 * 16; }  // tile-grid side
+__host__ __device__ inline int gt_rows(int64_t P) {  // window rows per LDS batch
+  const int64_t LX = (P + 15) / 16 * 16;
+  const int64_t rb = (96 * 1024 / 8 - 2 * LX) / LX;
+  return (int)std::min<int64_t>(16, std::max<int64_t>(4, rb & ~(int64_t)3));
+}
+__host__ __device__ inline int64_t adapt_gt_lds_bytes(int64_t P) {
+  const int64_t LX = (P + 15) / 16 * 16;
+  return ((int64_t)gt_rows(P) * LX + 2 * LX) * 8;
+}
+// tile k of the row-major upper triangle of an n x n tile grid starting at tile row r0 -> (ti, tj)
+__device__ __forceinline__ void tri_tile(int k, int n, int r0, int& ti, int& tj) {
+  int i = 0;
+  while (k >= n - i) {  // uniform
+    k -= n - i;
+    ++i;
+  }
+  ti = r0 + i;
+  tj = r0 + i + k;
+}
+
+__global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4))) void k_adapt_gt(DramState st,
+                                                                                                    DramParams p) {
+  constexpr int NW = kGtWaves, NTH = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  __shared__ int fail;
+  __shared__ double rdg[16];
+  __shared__ double Dt[256];  // U of the current panel's diagonal tile
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int row = lane & 15, kq = lane >> 4;
+  const int64_t c = blockIdx.x;
+  const int64_t step = *st.step;
+  if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
+  const int64_t ld = st.ld;
+  const int P = st.npar[c];
+  const int NT = (P + 15) >> 4, LX = 16 * NT, T = NT * (NT + 1) / 2;
+  const int rb = gt_rows(P);
+  double* X = dyn;           // a batch of centred window rows [rb][LX]
+  double* mb = X + rb * LX;  // batch mean
+  double* mo = mb + LX;      // old mean
+  double* cvg = st.cov + c * ld * ld;
+  double* mu = st.cmean + c * ld;
+  const int64_t LT = gt_lt(ld);
+  double* Wt = st.work + c * LT * LT;
+  auto tile = [&](int ti, int tj) { return Wt + ((int64_t)ti * NT + tj) * 256; };
+  const int nb = (int)p.adaptint;
+  const double* win = st.window + c * p.adaptint * ld;
+  for (int j = t; j < LX; j += NTH) {
+    mb[j] = j < P ? st.wsumv[c * ld + j] / (double)p.adaptint : 0.0;
+    mo[j] = j < P ? mu[j] : 0.0;
+  }
+  const double na = st.wsum[c], nn = na + (double)p.adaptint;
+  const double fcross = na * (double)p.adaptint / nn;
+  const double rn1 = 1.0 / (nn - 1.0);
+  // ---- covupd: scatter of the centred window rows + merge, kGtTiles tiles per wave and pass
+  for (int base = 0; base < T; base += NW * kGtTiles) {
+    int ti[kGtTiles], tj[kGtTiles];
+    bool val[kGtTiles];
+#pragma unroll
+    for (int g = 0; g < kGtTiles; ++g) {
+      const int k = base + w * kGtTiles + g;
+      val[g] = k < T;
+      tri_tile(val[g] ? k : 0, NT, 0, ti[g], tj[g]);
+    }
+    f64x4 acc[kGtTiles];
+#pragma unroll
+    for (int g = 0; g < kGtTiles; ++g) acc[g] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int r0 = 0; r0 < nb; r0 += rb) {
+      const int n = min(rb, nb - r0);
+      __syncthreads();  // the previous batch is consumed (and mb is written, first time)
+      for (int e = t; e < rb * LX; e += NTH) {
+        const int r = e / LX, j = e - r * LX;
+        X[e] = (r < n && j < P) ? win[(int64_t)(r0 + r) * ld + j] - mb[j] : 0.0;
+      }
+      __syncthreads();
+      for (int k0 = 0; k0 < n; k0 += 4) {
+        const double* xr = X + (k0 + kq) * LX + row;
+#pragma unroll
+        for (int g = 0; g < kGtTiles; ++g)
+          if (val[g]) acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr[16 * ti[g]], xr[16 * tj[g]], acc[g], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < kGtTiles; ++g) {
+      if (!val[g]) continue;  // uniform
+      double old[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // every old value of the tile before any write (mirrors)
+        const int i = 16 * ti[g] + kq + 4 * q, j = 16 * tj[g] + row;
+        old[q] = (i < P && j < P && na > 0.0) ? cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i] : 0.0;
+      }
+      double* A = tile(ti[g], tj[g]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 16 * ti[g] + kq + 4 * q, j = 16 * tj[g] + row;
+        double a;
+        if (i < P && j < P) {
+          double cv;
+          if (nn <= 1.0) {
+            cv = 0.0;  // a single row so far: covariance 0 (the recurrence's first row)
+          } else if (na == 0.0) {
+            cv = acc[g][q] * rn1;
+          } else {
+            const double di = mb[i] - mo[i], dj = mb[j] - mo[j];
+            cv = (old[q] * (na - 1.0) + acc[g][q] + di * dj * fcross) * rn1;
+          }
+          if (i <= j) cvg[(int64_t)i * ld + j] = cv;
+          a = cv + (i == j ? p.qcovadj : 0.0);
+        } else {
+          a = i == j ? 1.0 : 0.0;
+        }
+        A[(kq + 4 * q) * 16 + row] = a;
+      }
+    }
+  }
+  __syncthreads();  // mb / mo reads, tile writes
+  for (int j = t; j < P; j += NTH) mu[j] = na == 0.0 ? mb[j] : mo[j] + (mb[j] - mo[j]) * ((double)p.adaptint / nn);
+  if (t == 0) {
+    st.wsum[c] = nn;
+    fail = 0;
+  }
+  if (step < p.burnintime) {
+    // burn-in: no covariance adaptation, only scaling by the window's rejection rate
+    const double rate = (double)st.nrej_win[c] / (double)p.adaptint;
+    double s = 1.0;
+    if (rate > 0.95) s = 1.0 / p.burnin_scale;
+    else if (rate < 0.05) s = p.burnin_scale;
+    if (s != 1.0) {
+      double* R = st.R + c * ld * ld;
+      for (int64_t e = t; e < (int64_t)P * P; e += NTH) {
+        const int i = (int)(e / P), j = (int)(e % P);
+        store_R(st, c, P, i, j, f32_round(R[(int64_t)i * ld + j] * s));
+      }
+    }
+    __syncthreads();
+    if (t == 0) st.nrej_win[c] = 0;
+    return;
+  }
+  __syncthreads();
+  // ---- blocked Cholesky U'U of the tile grid
+  bool ok = true;
+  for (int pk = 0; pk < NT; ++pk) {
+    if (w == 0) {  // (1) the diagonal tile, factored in wave 0's registers
+      double* A = tile(pk, pk);
+      double dt[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dt[q] = A[(kq + 4 * q) * 16 + row];
+      bool bad = false;
+      chol16_step<0>(dt, lane, rdg, bad);
+      wave_sync();
+      chol16_finish(dt, lane, rdg, rdg);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        A[(kq + 4 * q) * 16 + row] = dt[q];
+        Dt[(kq + 4 * q) * 16 + row] = dt[q];
+      }
+      if (bad && lane == 0) fail = 1;
+    }
+    __syncthreads();
+    if (fail) {
+      ok = false;
+      break;
+    }
+    {  // (2) the panel's row tiles (pk, tj > pk): U_pk' X = A -> X, one column per lane
+      const int g = w * 4 + kq;  // 16-lane group 0 .. 4 NW - 1
+      for (int tj = pk + 1 + g; tj < NT; tj += 4 * NW) {
+        asm volatile("" ::: "memory");  // Dt is re-read per tile, not hoisted into 120 registers
+        double* A = tile(pk, tj);
+        double x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = A[k * 16 + row];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          x[k] = x[k] * rdg[k];
+#pragma unroll
+          for (int m = k + 1; m < 16; ++m) x[m] = fma(-Dt[k * 16 + m], x[k], x[m]);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) A[k * 16 + row] = x[k];
+      }
+    }
+    __syncthreads();
+    {  // (3) trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj (4 MFMAs), round-robin over waves
+      const int m = NT - pk - 1, Ttr = m * (m + 1) / 2;
+      for (int k = w; k < Ttr; k += NW) {
+        int ti, tj;
+        tri_tile(k, m, pk + 1, ti, tj);
+        double* A = tile(ti, tj);
+        const double* Xi = tile(pk, ti);
+        const double* Xj = tile(pk, tj);
+        f64x4 acc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = A[(kq + 4 * q) * 16 + row];
+#pragma unroll
+        for (int k4 = 0; k4 < 16; k4 += 4)
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Xi[(k4 + kq) * 16 + row], Xj[(k4 + kq) * 16 + row], acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) A[(kq + 4 * q) * 16 + row] = acc[q];
+      }
+    }
+    __syncthreads();
+  }
+  if (ok) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
+    const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
+    for (int k = w; k < T; k += NW) {
+      int ti, tj;
+      tri_tile(k, NT, 0, ti, tj);
+      const double* A = tile(ti, tj);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 16 * ti + kq + 4 * q, j = 16 * tj + row;
+        if (i < P && j < P && j >= i) store_R(st, c, P, i, j, f32_round(A[(kq + 4 * q) * 16 + row] * sc));
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) st.nrej_win[c] = 0;
+}
+
 inline int finish() { return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP; }
 inline dim3 chain_grid(int64_t n) { return dim3((unsigned)n); }
 
@@ -1838,11 +1978,11 @@ int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
 #else
   if (p.pmax <= 16 * 13) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
 #endif
-  const size_t lds = p.lds_matrix ? (size_t)p.lds_matrix : 0;
-  if (lds > 0 && hipFuncSetAttribute((const void*)k_adapt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-                     hipSuccess)
+  const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax);
+  if (lds > 48 * 1024 &&
+      hipFuncSetAttribute((const void*)k_adapt_gt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return TCI_EHIP;
-  hipLaunchKernelGGL(k_adapt, chain_grid(st.n_chains), dim3(kThreads), lds, (hipStream_t)stream, st, p);
+  hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.n_chains), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);
   return finish();
 }
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,

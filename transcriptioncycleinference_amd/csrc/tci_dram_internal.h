@@ -51,7 +51,7 @@ struct DramState {
   double* sq_m2;
   double* chain_out;       // optional thinned chain rows (n_keep x n_chains x ld) or null
   double* s2_out;          // optional thinned s2 rows
-  double* work;            // Cholesky workspace (n_chains x ld x ld)
+  double* work;            // Cholesky tile grid of k_adapt_gt (n_chains x gt_lt(ld)^2)
   int64_t* step;           // current chain row (1-based), advanced on device after each step
   int64_t* prof;           // TCI_CHAIN_PROFILE builds only: k_chain phase cycles, summed over chains
   double* draws;           // fused engine: per chain, p.chunk rows of draw_stride(ld) doubles (k_draws)
@@ -74,7 +74,6 @@ struct DramParams {
   int64_t stats_from;
   int64_t thin;
   int64_t n_keep;
-  int64_t lds_matrix;  // bytes of dynamic LDS for the adaptation matrix (0 = work in global memory)
   int64_t pmax;        // max parameter count over the chains (picks the adaptation kernel)
   int64_t chunk;       // fused engine: rows per chain of the draws buffer (>= the longest chunk)
   int64_t walk;        // fused engine: 1 = one wavefront per chain walks the chunk (k_walk), 0 = k_chain
