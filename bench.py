@@ -436,6 +436,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true", help="skip the K in {1, 64, 256, 1024} kernel sweep")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the drop-in latency and host-pointer legs (profiling runs: only the K launch)")
     ap.add_argument("--dram-steps", type=int, default=200000,
                     help="end-to-end mode: one DRAM chain per TestData cell for this many steps (0 = skip)")
     ap.add_argument("--no-configs", action="store_true",
@@ -548,7 +550,7 @@ def main():
         res["kernel_sweep"] = kernel_sweep(lk, cells, dev, stream, seed=77 + rank)
     theta_h = rounds.theta[0].cpu().numpy()
     act_h = rounds.active[0].cpu().numpy()
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_latency:
         res["drop_in_latency"] = drop_in_latency(lk, cells, theta_h, rounds.cid_host)
         # PCIe-inclusive rate of the host-pointer entry point for the whole K-proposal batch
         # (theta H2D + SS D2H per call): reported beside, never as, `value`.

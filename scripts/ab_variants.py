@@ -19,20 +19,23 @@ VARIANTS = {
     "old": None,  # a prebuilt library of the previous commit, copied to build/ab/libtci_old.so
     "adapt16": ["TCI_ADAPT_WAVES13=16"],
     "abl_rows": ["TCI_ABLATE=1"],
-    "abl_bounds": ["TCI_ABLATE=2"],
     "abl_interp": ["TCI_ABLATE=4"],
     "abl_scan": ["TCI_ABLATE=8"],
     "abl_all": ["TCI_ABLATE=15"],
-    "w6_noxcd": ["TCI_WAVES_PER_EU=6", "TCI_XCD_REMAP=0"],
     "w8_latepts": ["TCI_WAVES_PER_EU=8", "TCI_EARLY_POINTS=0"],
-    "loopramp": ["TCI_RAMP_PREFIX=0"],
     "abl_loads": ["TCI_ABLATE=16"],
+    "abl_launch": ["TCI_ABLATE=32"],
+    "wpb1": ["TCI_WAVES_PER_BLOCK=1"],
+    "wpb8": ["TCI_WAVES_PER_BLOCK=8"],
+    "w8": ["TCI_WAVES_PER_EU=8"],
     "chainprof": ["TCI_CHAIN_PROFILE=1"],
     "chainprof2": ["TCI_CHAIN_PROFILE=2"],
     "rec2_s3": ["TCI_REC_WAVE=2", "TCI_S2_WAVE=3"],
     "rec2_s2": ["TCI_REC_WAVE=2", "TCI_S2_WAVE=2"],
     "rec3_s2": ["TCI_REC_WAVE=3", "TCI_S2_WAVE=2"],
     "normal_f32": ["TCI_NORMAL_F32=1"],
+    "normal_f64": ["TCI_NORMAL_F32=0"],
+    "r02a": None,  # a prebuilt library of commit 8540df6
     "adaptprof": ["TCI_ADAPT_PROFILE=1"],
     "adapt_twice": ["TCI_ADAPT_TWICE=1"],
     "adapt_nochol": ["TCI_ADAPT_ABLATE=1"],

@@ -167,6 +167,9 @@ int pick_rpl(int64_t max_points) {
 int run(tci_ctx* ctx, int mode, const double* theta, int64_t ld, const int32_t* cell, const uint8_t* active,
         int64_t B, double* out0, double* out1, int64_t ld_out, void* stream) {
   TCI_HIP(ctx, hipSetDevice(ctx->device));
+  // every cell has >= 2 points, so a row needs >= 9 entries; the kernels read theta[0..6] of a row
+  // before they know its cell (tci_kernels.hip)
+  if (B > 0 && ld < 9) return fail(ctx, TCI_ERANGE, "ld_theta=" + std::to_string(ld) + " < 9 (7 + at least 2 rates)");
   const int rc = tci::launch(ctx->kp, ctx->rpl, mode, theta, ld, cell, active, B, out0, out1, ld_out, stream);
   if (rc != TCI_OK) {
     if (rc == TCI_EHIP) return hip_fail(ctx, hipGetLastError(), "kernel launch");

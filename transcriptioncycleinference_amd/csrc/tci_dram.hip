@@ -164,8 +164,6 @@ __device__ __forceinline__ double lane_bcast(double x, int l) {
   return __hiloint2double(hi, lo);
 }
 
-constexpr int kVec = TCI_MAX_POINTS + 8;
-
 // Acceptance terms shared by every engine (the same expressions, so the same bits):
 //   log of a Metropolis ratio  -0.5*(ss_new - ss_old)/s2 - 0.5*(prior_new - prior_old), with the
 //   division by s2 taken as a product with the precision ip = 1/s2 (computed once per state);
@@ -883,16 +881,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   }
   EvalIn<RPL> e;  // the chain's cell records stay in registers
   {
-    const int cell = st.cell[c];
-    const int64_t cbase = (int64_t)cell * kp.cell_stride;
-    e.cm = kp.cells[cell];
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) e.st[q] = kp.steps[cbase + RPL * lane + q];
-#pragma unroll
-    for (int k = 0; k <= RPL; ++k) {
-      const int j = lane + 64 * k;
-      e.pt[k] = j <= 64 * RPL ? kp.points[cbase + j] : PointRec{NAN, NAN, NAN, 0, 0};
-    }
+    load_cell<RPL, false>(kp, st.cell[c], lane, e);
   }
   double ss = st.ss[c], prior = st.prior[c];
   // sigma2 chain (kSigWave): s2 of the last decided row, or its Gamma variate Gl while that s2
@@ -1184,16 +1173,7 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
   }
   EvalIn<RPL> e;  // the chain's cell records stay in registers
   {
-    const int cell = st.cell[c];
-    const int64_t cbase = (int64_t)cell * kp.cell_stride;
-    e.cm = kp.cells[cell];
-#pragma unroll
-    for (int q = 0; q < RPL; ++q) e.st[q] = kp.steps[cbase + RPL * lane + q];
-#pragma unroll
-    for (int k = 0; k <= RPL; ++k) {
-      const int j = lane + 64 * k;
-      e.pt[k] = j <= 64 * RPL ? kp.points[cbase + j] : PointRec{NAN, NAN, NAN, 0, 0};
-    }
+    load_cell<RPL, false>(kp, st.cell[c], lane, e);
   }
   double ss = st.ss[c], prior = st.prior[c], s2 = st.sigma2[c];
   S2Stats s2a{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};

@@ -52,12 +52,9 @@
 #include "tci_internal.h"
 
 // Build-time variants for A/B timing (scripts/ab_variants.py); the shipped defaults are below.
-#ifndef TCI_RAMP_PREFIX
-#define TCI_RAMP_PREFIX 1    // O(1) ramp via the J prefix table (else a loop over ramp distances)
-#endif
 #ifndef TCI_ABLATE
-#define TCI_ABLATE 0         // diagnostics only (wrong results): bit0 rows, bit1 bounds, bit2 interp, bit3 scan,
-#endif                       // bit4 loads only
+#define TCI_ABLATE 0         // diagnostics only (wrong results): bit0 rows, bit2 interp, bit3 scan, bit4 loads only, bit5 launch only
+#endif
 
 namespace tci {
 
@@ -130,11 +127,74 @@ __device__ __forceinline__ double occupancy(double p, const SegParams& s, double
   return p < s.e ? fr : full;
 }
 
-// Distance-table regions of one segment of one dye: ramp m in [r_lo, r_hi] (a < P_m < e),
-// full m in [f_lo, f_hi] (e < P_m < L). Empty ranges have lo > hi.
-struct Regions {
-  int r_lo, r_hi, f_lo, f_hi;
+// Distance cut of one threshold x on the fast path: n(x) = #{m in [1, nsteps] : P_m < x}, where
+// P_m = m * vd0 is the representative position m steps after loading (P_m is monotone in m).
+// The cuts of all thresholds are computed at once, one threshold per lane, from x / vd0 and four
+// exact candidate products around it, instead of one vote per (slot, threshold):
+//   m_c = clamp(floor(x * rcp(vd0)) - 1, -2, nsteps + 1),  candidates m_c .. m_c + 3,
+//   n(x) = clamp(m_c - 1 + #{candidates with P_m < x}, 0, nsteps).
+// That count is exact whenever P_{m_c} < x (or m_c <= 0) and P_{m_c+3} >= x (or m_c + 3 > nsteps);
+// |x * rcp(vd0) - x / vd0| << 1 for every m that can matter, and a candidate set that does not
+// bracket x is flagged instead of trusted. `bad` also flags a candidate in [1, nsteps] within
+// eps of x: the same exactness test as one vote per m, because every other P_m is at least
+// ~vd0 > 4 eps away from x (eps >= vd0/4 is flagged too). A flagged wave takes the exact sweep.
+__device__ __forceinline__ int distance_cut(double x, double vd0, double rvd0, double eps, int nsteps, bool& bad) {
+  const double mf = x > 0.0 ? x * rvd0 : 0.0;  // x <= 0: no P_m (m >= 1) lies below it
+  double mc = floor(mf) - 1.0;
+  mc = mc > -2.0 ? mc : -2.0;
+  mc = mc < (double)(nsteps + 1) ? mc : (double)(nsteps + 1);  // also +Inf / NaN (rcp of a denormal)
+  const int m0 = (int)mc;
+  int cnt = m0 - 1;
+  bool near = !(eps < 0.25 * vd0);
+  bool l0 = false, l3 = false;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + j;
+    const double P = (double)m * vd0;  // the same product as P_m = (g + 1) * vd0 per slot
+    const bool lt = P < x;
+    cnt += lt ? 1 : 0;
+    near = near | (m >= 1 && m <= nsteps && fabs(P - x) <= eps);
+    if (j == 0) l0 = lt;
+    if (j == 3) l3 = lt;
+  }
+  bad = near || (!l0 && m0 >= 1) || (l3 && m0 + 3 <= nsteps);
+  return min(max(cnt, 0), nsteps);
+}
+
+// Cuts of one evaluation (wave-uniform, SGPRs): nL = n(L); per segment and dye na = n(a), ne = n(e).
+// The row sums need only three table entries per (segment, dye) and one shared one (row_sum).
+template <int NSEG>
+struct Cuts {
+  int nL;
+  int nMa[NSEG], nMe[NSEG], nPa[NSEG], nPe[NSEG];
 };
+
+// Lane j holds threshold j: 0 -> L, 1 + 4k .. 4 + 4k -> MS2 a, MS2 e, PP7 a, PP7 e of segment k.
+// Returns false (take the exact sweep) when any cut is flagged.
+template <int NSEG>
+__device__ __forceinline__ bool distance_cuts(const SegParams* sm, const SegParams* sp, double L, double vd0,
+                                              double eps, int nsteps, int lane, Cuts<NSEG>& cu) {
+  double x = L;
+#pragma unroll
+  for (int k = 0; k < NSEG; ++k) {
+    x = lane == 1 + 4 * k ? sm[k].a : x;
+    x = lane == 2 + 4 * k ? sm[k].e : x;
+    x = lane == 3 + 4 * k ? sp[k].a : x;
+    x = lane == 4 + 4 * k ? sp[k].e : x;
+  }
+  bool bad;
+  const int cnt = distance_cut(x, vd0, __builtin_amdgcn_rcp(vd0), eps, nsteps, bad);
+  constexpr uint64_t used = (1ull << (1 + 4 * NSEG)) - 1;
+  cu.nL = __builtin_amdgcn_readlane(cnt, 0);
+#pragma unroll
+  for (int k = 0; k < NSEG; ++k) {
+    cu.nMa[k] = __builtin_amdgcn_readlane(cnt, 1 + 4 * k);
+    cu.nMe[k] = __builtin_amdgcn_readlane(cnt, 2 + 4 * k);
+    cu.nPa[k] = __builtin_amdgcn_readlane(cnt, 3 + 4 * k);
+    cu.nPe[k] = __builtin_amdgcn_readlane(cnt, 4 + 4 * k);
+  }
+  return (wave_ballot(bad) & used) == 0;
+}
 
 // Exact prefix tables of the fast path, interleaved per cohort index i (LDS, 16 B per entry):
 //   K_i = sum_{i' <= i} c_i'        (= floor(counter_i): polymerases loaded through step i)
@@ -145,32 +205,23 @@ struct Regions {
 template <bool CLAMP = false>
 __device__ __forceinline__ double2 kj_at(const double2* KJ, int i) { return KJ[CLAMP ? max(i, -1) : i]; }
 
-// Row sum of one segment of one dye on the fast path (see the header), O(1) per row:
-//   full  (e < P_m < L, m in [f_lo, f_hi]):  phi * (K[r - f_lo] - K[r - f_hi - 1])
-//   ramp  (a < P_m < e, m in [r_lo, r_hi]):  sum_m c_{r-m} * (m*vd0 - a) * k
-//        = (k*vd0) * sum_m m*c_{r-m}  -  (k*a) * sum_m c_{r-m},   sum_m m*c_{r-m} = r*C - (J_hi - J_lo)
-// kvd = k*vd0 and ka = k*a are wave constants; C, J differences and r*C - dJ are exact integers.
+// Row sum of one segment of one dye on the fast path (see the header), O(1) per row, from the
+// cuts na = n(a), ne = n(e), nL = n(L):
+//   full  (e < P_m < L, m in [ne + 1, nL]):  phi * (K[r - ne - 1] - K[r - nL - 1])   (kL = K[r - nL - 1])
+//   ramp  (a < P_m < e, m in [na + 1, ne]):  sum_m c_{r-m} * (m*vd0 - a) * k
+//        = (k*vd0) * sum_m m*c_{r-m}  -  (k*a) * sum_m c_{r-m},   sum_m m*c_{r-m} = r*C - (J_A - J_E)
+// with A = KJ[r - na - 1], E = KJ[r - ne - 1]. kvd = k*vd0 and ka = k*a are wave constants; C, the
+// J difference and r*C - dJ are exact integers. Branch-free, so every table read of a row issues
+// at once: an empty ramp (na == ne) reads A == E and adds exactly 0; an empty full region
+// (ne >= nL) has K[r - ne - 1] <= kL and max(., 0) makes it exactly 0, as skipping it would.
 template <bool CLAMP = false>
-__device__ __forceinline__ double row_sum(const double2* KJ, int r, double rd, const Regions& rg,
+__device__ __forceinline__ double row_sum(const double2* KJ, int r, double rd, int na, int ne, double kL,
                                           const SegParams& s, double kvd, double ka) {
-  double acc = 0.0;
-  if (rg.f_lo <= rg.f_hi) acc = s.phi * (kj_at<CLAMP>(KJ, r - rg.f_lo).x - kj_at<CLAMP>(KJ, r - rg.f_hi - 1).x);
-  if (rg.r_lo <= rg.r_hi) {
-#if TCI_RAMP_PREFIX
-    const double2 hi = kj_at<CLAMP>(KJ, r - rg.r_lo), lo = kj_at<CLAMP>(KJ, r - rg.r_hi - 1);
-    const double C = hi.x - lo.x;
-    const double Mc = fma(rd, C, -(hi.y - lo.y));  // sum of m * c_{r-m}, exact
-    acc = fma(kvd, Mc, fma(-ka, C, acc));
-#else
-    double kA = kj_at<CLAMP>(KJ, r - rg.r_lo).x;
-    for (int m = rg.r_lo; m <= rg.r_hi; ++m) {
-      const double kB = kj_at<CLAMP>(KJ, r - m - 1).x;
-      acc = fma(kA - kB, fma((double)m, kvd, -ka), acc);
-      kA = kB;
-    }
-#endif
-  }
-  return acc;
+  const double2 A = kj_at<CLAMP>(KJ, r - na - 1), E = kj_at<CLAMP>(KJ, r - ne - 1);
+  const double full = s.phi * fmax(E.x - kL, 0.0);
+  const double C = A.x - E.x;
+  const double Mc = fma(rd, C, -(A.y - E.y));  // sum of m * c_{r-m}, exact
+  return fma(kvd, Mc, fma(-ka, C, full));
 }
 
 template <int MODE>
@@ -199,6 +250,27 @@ struct EvalIn {
   StepRec st[RPL];
   PointRec pt[RPL + 1];               // points lane + 64*k (the last one only for lane 0)
 };
+
+// The cell's records into registers: lane l holds steps RPL*l .. RPL*l + RPL - 1 and points
+// l + 64*k. RAW: the raw-time steps (forward model on raw t). A point past 64*RPL (only
+// N = 64*RPL + 1 has one, on lane 0) is read only where it exists in the table.
+template <int RPL, bool RAW>
+__device__ __forceinline__ void load_cell(const KParams& kp, int c, int lane, EvalIn<RPL>& e) {
+  const int64_t cbase = (int64_t)c * kp.cell_stride;
+  const StepRec* ST = (RAW ? kp.steps_raw : kp.steps) + cbase;
+  const PointRec* PT = kp.points + cbase;
+  e.cm = kp.cells[c];
+#pragma unroll
+  for (int q = 0; q < RPL; ++q) e.st[q] = ST[RPL * lane + q];  // < cell_stride
+  if (!RAW) {
+#pragma unroll
+    for (int k = 0; k <= RPL; ++k) {
+      const int j = lane + 64 * k;
+      if (k < RPL || j <= 64 * RPL) e.pt[k] = PT[j];
+      else e.pt[k] = PointRec{NAN, NAN, NAN, 0, 0};  // beyond every cell's points: dropped
+    }
+  }
+}
 
 // One ssfun evaluation (MODE_SS: returns the SS, wave-uniform) or forward model (rows written
 // to out0/out1 row b) by one wavefront, on its LDS (2 * (2*64*RPL + 2*RPL) doubles). Needs
@@ -316,57 +388,13 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
   if (v > 0.0) {
     bool fast = MODE != MODE_FWD_RAW && !(kp.force_exact & 2);
     const double vd0 = v * cm.d;
-    Regions rgM[NSEG], rgP[NSEG];
-#if TCI_ABLATE & 2
-    if (fast) {
-#pragma unroll
-      for (int k = 0; k < NSEG; ++k) {
-        const int m0 = (int)(sm[k].a / vd0);
-        rgM[k] = Regions{m0 + 1, m0 + 4, m0 + 5, m0 + 20};
-        rgP[k] = Regions{m0 + 9, m0 + 12, m0 + 13, m0 + 20};
-      }
-    }
-    if (false) {
-#else
-    if (fast) {
-#endif
-      // ---- distance regions and their exactness proof
-      // |p(r, r-m) - P_m| <= v * (m*delta + (m+4)*u*m*(d+delta)) for every m <= nsteps; eps is
-      // twice that at m = nsteps, precomputed per cell up to the factor v (CellMeta::eps_v)
-      const double eps = v * cm.eps_v;
-      uint64_t amb = 0;
-      int n_lt_L = 0;
-      // No P_m equals a threshold unless it is within eps > 0 of it (then the wave goes exact),
-      // so on the fast path #(P_m <= x) == #(P_m < x) and one count per threshold suffices.
-      int nM_a[NSEG], nM_e[NSEG], nP_a[NSEG], nP_e[NSEG];
-#pragma unroll
-      for (int k = 0; k < NSEG; ++k) nM_a[k] = nM_e[k] = nP_a[k] = nP_e[k] = 0;
-#pragma unroll
-      for (int q = 0; q < RPL; ++q) {
-        const int g = RPL * lane + q;
-        const uint64_t vmask = step_lanes<RPL>(nsteps, q);  // AND-ed on the scalar unit, not per vote
-        const double md = (double)(g + 1);
-        const double Pm = md * vd0;
-        bool near = fabs(Pm - L) <= eps;
-        n_lt_L += __popcll(vmask & wave_ballot(Pm < L));
-#pragma unroll
-        for (int k = 0; k < NSEG; ++k) {
-          near = near | (fabs(Pm - sm[k].a) <= eps) | (fabs(Pm - sm[k].e) <= eps) | (fabs(Pm - sp[k].a) <= eps) |
-                 (fabs(Pm - sp[k].e) <= eps);
-          nM_a[k] += __popcll(vmask & wave_ballot(Pm < sm[k].a));
-          nM_e[k] += __popcll(vmask & wave_ballot(Pm < sm[k].e));
-          nP_a[k] += __popcll(vmask & wave_ballot(Pm < sp[k].a));
-          nP_e[k] += __popcll(vmask & wave_ballot(Pm < sp[k].e));
-        }
-        amb |= vmask & wave_ballot(near);
-      }
-      fast = amb == 0;
-#pragma unroll
-      for (int k = 0; k < NSEG; ++k) {
-        rgM[k] = Regions{nM_a[k] + 1, nM_e[k], nM_e[k] + 1, n_lt_L};
-        rgP[k] = Regions{nP_a[k] + 1, nP_e[k], nP_e[k] + 1, n_lt_L};
-      }
-    }
+    Cuts<NSEG> cu;
+    // ---- distance cuts and their exactness proof (distance_cut)
+    // |p(r, r-m) - P_m| <= v * (m*delta + (m+4)*u*m*(d+delta)) for every m <= nsteps; eps is
+    // twice that at m = nsteps, precomputed per cell up to the factor v (CellMeta::eps_v).
+    // No P_m equals a threshold unless it is within eps > 0 of it (then the wave goes exact),
+    // so on the fast path #(P_m <= x) == #(P_m < x) and one count per threshold suffices.
+    if (fast) fast = distance_cuts<NSEG>(sm, sp, L, vd0, v * cm.eps_v, nsteps, lane, cu);
     if (fast) {
       // ---- {K, J} prefix tables (exact) and O(1) row sums
       double jloc[RPL], js = 0.0;
@@ -402,16 +430,21 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
       for (int q = 0; q < RPL; ++q) {
         const int r = RPL * lane + q + 1;
         const double rd = (double)r;
+        const double kL = KJ[r - cu.nL - 1].x;  // shared by every segment and dye (L_MS2 = L_PP7)
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) {
 #if TCI_ABLATE & 1
-          accM[k][q] = KJ[r].x + (double)rgM[k].f_lo;
-          accP[k][q] = KJ[r].y + (double)rgP[k].f_hi;
+          accM[k][q] = KJ[r].x + (double)cu.nMa[k];
+          accP[k][q] = KJ[r].y + (double)cu.nL;
 #else
-          accM[k][q] = row_sum(KJ, r, rd, rgM[k], sm[k], kvdM[k], kaM[k]);
-          accP[k][q] = row_sum(KJ, r, rd, rgP[k], sp[k], kvdP[k], kaP[k]);
+          accM[k][q] = row_sum(KJ, r, rd, cu.nMa[k], cu.nMe[k], kL, sm[k], kvdM[k], kaM[k]);
+          accP[k][q] = row_sum(KJ, r, rd, cu.nPa[k], cu.nPe[k], kL, sp[k], kvdP[k], kaP[k]);
 #endif
         }
+        // one row's table reads in flight at a time: issued all at once, the 4*NSEG + 1 reads of
+        // every row would hold 16 VGPRs per (row, segment) and push the register-bound chain
+        // kernels (tci_dram.hip) into spills
+        if (RPL * NSEG > 2) __builtin_amdgcn_sched_barrier(0);
       }
     } else {
       // ---- exact systolic sweep: at iteration s slot g holds cohort g-s+1 with its forward position

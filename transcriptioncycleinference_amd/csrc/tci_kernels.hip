@@ -9,6 +9,9 @@
 #ifndef TCI_WAVES_PER_EU
 #define TCI_WAVES_PER_EU 6   // register budget for 6 waves/SIMD (A/B: 50 us vs 58 us at the
 #endif                       // compiler's default 5 waves; 7-8 waves no faster)
+#ifndef TCI_WAVES_PER_BLOCK
+#define TCI_WAVES_PER_BLOCK 4
+#endif
 #if TCI_WAVES_PER_EU > 0
 #define TCI_OCCUPANCY __attribute__((amdgpu_waves_per_eu(TCI_WAVES_PER_EU)))
 #else
@@ -19,16 +22,14 @@ namespace tci {
 
 namespace {
 
-constexpr int kWavesPerBlock = 4;
+constexpr int kWavesPerBlock = TCI_WAVES_PER_BLOCK;
 
 template <int RPL, int NSEG, int MODE>
-__global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
+__global__ __launch_bounds__(64 * TCI_WAVES_PER_BLOCK) TCI_OCCUPANCY void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
                                                          int64_t ld_out) {
-  constexpr int SLOTS = 64 * RPL;      // rows 1..SLOTS (row 0 never holds a polymerase)
-  constexpr int NPT = RPL + 1;         // acquisition points per lane (N <= 64*RPL + 1)
   constexpr int WAVE_DOUBLES = eval_lds_doubles<RPL>();  // {K,J} table / the two sim rows
   __shared__ __attribute__((aligned(16))) double s_lds[kWavesPerBlock][WAVE_DOUBLES];
 
@@ -46,9 +47,23 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
   const int64_t b = (int64_t)vb * kWavesPerBlock + wid;
   if (b >= B) return;
   double* lds = s_lds[wid];
+#if TCI_ABLATE & 32
+  if (lane == 0) out0[b] = 1.0;  // launch floor (diagnostics only)
+  return;
+#endif
 
-  // ---- every load of the evaluation is issued here, in one round trip
+  // ---- round trip 1: what the row index alone addresses -- the cell id, the active flag and the
+  //      wave-uniform theta entries (ld >= 9 is checked by the host, so th[0..6] is inside the row)
   const int c = __builtin_amdgcn_readfirstlane(cell_id[b]);
+  const double* th = theta + b * ld;
+  EvalIn<RPL> e;
+  e.v = th[0];
+  e.tau = th[1];
+  e.ton = th[2];
+  e.b1 = th[3];
+  e.b2 = th[4];
+  e.A = th[5];
+  e.R = th[6];
   const bool act = MODE != MODE_SS || active == nullptr || active[b] != 0;
   if (!act) {
     if (lane == 0) out0[b] = INFINITY;  // skipped proposal (bounds-rejected by the caller)
@@ -58,40 +73,24 @@ __global__ __launch_bounds__(256) TCI_OCCUPANCY void tci_cohort_kernel(const KPa
     write_nan<MODE>(lane, 0, b, out0, out1, ld_out);
     return;
   }
-  const int64_t cbase = (int64_t)c * kp.cell_stride;
-  const StepRec* ST = (MODE == MODE_FWD_RAW ? kp.steps_raw : kp.steps) + cbase;
-  const PointRec* PT = kp.points + cbase;
-  const double* th = theta + b * ld;
-  EvalIn<RPL> e;
-  e.cm = kp.cells[c];
-  e.v = th[0];
-  e.tau = th[1];
-  e.ton = th[2];
-  e.b1 = th[3];
-  e.b2 = th[4];
-  e.A = th[5];
-  e.R = th[6];
+  // ---- round trip 2: the cell's records and the row's dR entries
+  load_cell<RPL, MODE == MODE_FWD_RAW>(kp, c, lane, e);
 #pragma unroll
   for (int q = 0; q < RPL; ++q) {
     const int g = RPL * lane + q;
     e.dr[q] = 7 + g < ld ? th[7 + g] : 0.0;  // speculative (N unknown yet), kept inside the row
-    e.st[q] = ST[g];                          // g < cell_stride
-  }
-  if (MODE != MODE_FWD_RAW) {
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int j = lane + 64 * k;
-      if (j <= SLOTS) e.pt[k] = PT[j];
-      else e.pt[k] = PointRec{NAN, NAN, NAN, 0, 0};  // beyond every cell's points: dropped
-    }
   }
   const int N = e.cm.n;
-  if (ld < 7 + N) {
+  // A row shorter than 7 + N gives NaN. SS mode decides that after the evaluation (the dR loads
+  // above stay inside the row either way): a branch on N here would hold back the theta loads
+  // until the cell record has arrived, one more round trip.
+  const bool short_row = ld < 7 + N;
+  if (MODE != MODE_SS && short_row) {
     write_nan<MODE>(lane, N, b, out0, out1, ld_out);
     return;
   }
   const double ss = eval_wave<RPL, NSEG, MODE>(kp, e, lane, lds, b, out0, out1, ld_out);
-  if (MODE == MODE_SS && lane == 0) out0[b] = ss;
+  if (MODE == MODE_SS && lane == 0) out0[b] = short_row ? NAN : ss;
 }
 
 template <int RPL, int NSEG, int MODE>
@@ -253,39 +252,9 @@ __global__ __launch_bounds__(64) void tci_tile_kernel(const KParams kp, const do
 
   bool fast = MODE != MODE_FWD_RAW && !(kp.force_exact & 2);
   const double vd0 = v * cm.d;
-  Regions rgM[NSEG], rgP[NSEG];
-  if (v > 0.0 && fast) {
-    // ---- distance regions over m = 1..S and their exactness proof (as eval_wave)
-    const double eps = v * cm.eps_v;
-    uint64_t ambr = 0;
-    int n_lt_L = 0;
-    int nM_a[NSEG], nM_e[NSEG], nP_a[NSEG], nP_e[NSEG];
-#pragma unroll
-    for (int k = 0; k < NSEG; ++k) nM_a[k] = nM_e[k] = nP_a[k] = nP_e[k] = 0;
-    for (int g0 = 0; g0 < S; g0 += 64) {
-      const int g = g0 + lane;
-      const uint64_t vmask = S - g0 >= 64 ? ~0ull : (1ull << (S - g0)) - 1;
-      const double Pm = (double)(g + 1) * vd0;
-      bool near = fabs(Pm - L) <= eps;
-      n_lt_L += __popcll(vmask & wave_ballot(Pm < L));
-#pragma unroll
-      for (int k = 0; k < NSEG; ++k) {
-        near = near | (fabs(Pm - sm[k].a) <= eps) | (fabs(Pm - sm[k].e) <= eps) | (fabs(Pm - sp[k].a) <= eps) |
-               (fabs(Pm - sp[k].e) <= eps);
-        nM_a[k] += __popcll(vmask & wave_ballot(Pm < sm[k].a));
-        nM_e[k] += __popcll(vmask & wave_ballot(Pm < sm[k].e));
-        nP_a[k] += __popcll(vmask & wave_ballot(Pm < sp[k].a));
-        nP_e[k] += __popcll(vmask & wave_ballot(Pm < sp[k].e));
-      }
-      ambr |= vmask & wave_ballot(near);
-    }
-    fast = ambr == 0;
-#pragma unroll
-    for (int k = 0; k < NSEG; ++k) {
-      rgM[k] = Regions{nM_a[k] + 1, nM_e[k], nM_e[k] + 1, n_lt_L};
-      rgP[k] = Regions{nP_a[k] + 1, nP_e[k], nP_e[k] + 1, n_lt_L};
-    }
-  }
+  Cuts<NSEG> cu;
+  // ---- distance cuts over m = 1..S and their exactness proof (as eval_wave)
+  if (v > 0.0 && fast) fast = distance_cuts<NSEG>(sm, sp, L, vd0, v * cm.eps_v, S, lane, cu);
   if (v > 0.0 && fast) {
     // ---- O(1) row sums from the {K, J} tables, floors inside the segment loop, x A
     double kvdM[NSEG], kaM[NSEG], kvdP[NSEG], kaP[NSEG];
@@ -300,11 +269,12 @@ __global__ __launch_bounds__(64) void tci_tile_kernel(const KParams kp, const do
       const int r = r0 + lane;
       if (r > S) break;
       const double rd = (double)r;
+      const double kL = kj_at<true>(KJ, r - cu.nL - 1).x;
       double m = 0.0, pp = 0.0;
 #pragma unroll
       for (int k = 0; k < NSEG; ++k) {
-        const double aM = row_sum<true>(KJ, r, rd, rgM[k], sm[k], kvdM[k], kaM[k]);
-        const double aP = row_sum<true>(KJ, r, rd, rgP[k], sp[k], kvdP[k], kaP[k]);
+        const double aM = row_sum<true>(KJ, r, rd, cu.nMa[k], cu.nMe[k], kL, sm[k], kvdM[k], kaM[k]);
+        const double aP = row_sum<true>(KJ, r, rd, cu.nPa[k], cu.nPe[k], kL, sp[k], kvdP[k], kaP[k]);
         m = k == 0 ? fmax(aM, b1) : fmax(m + aM, b1);
         pp = k == 0 ? fmax(aP, b2) : fmax(pp + aP, b2);
       }
