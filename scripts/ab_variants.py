@@ -30,12 +30,16 @@ VARIANTS = {
     "w8": ["TCI_WAVES_PER_EU=8"],
     "chainprof": ["TCI_CHAIN_PROFILE=1"],
     "chainprof2": ["TCI_CHAIN_PROFILE=2"],
-    "rec2_s3": ["TCI_REC_WAVE=2", "TCI_S2_WAVE=3"],
-    "rec2_s2": ["TCI_REC_WAVE=2", "TCI_S2_WAVE=2"],
-    "rec3_s2": ["TCI_REC_WAVE=3", "TCI_S2_WAVE=2"],
+    "rec1_s3": ["TCI_REC_WAVE=1", "TCI_SIG_WAVE=3"],
+    "rec3_s1": ["TCI_REC_WAVE=3", "TCI_SIG_WAVE=1"],
+    "rec1_s2": ["TCI_REC_WAVE=1", "TCI_SIG_WAVE=2"],
+    "rec0_s3": ["TCI_REC_WAVE=0", "TCI_SIG_WAVE=3"],
+    "rec0_s1": ["TCI_REC_WAVE=0", "TCI_SIG_WAVE=1"],
+    "rec2_s0": ["TCI_REC_WAVE=2", "TCI_SIG_WAVE=0"],
     "normal_f32": ["TCI_NORMAL_F32=1"],
     "normal_f64": ["TCI_NORMAL_F32=0"],
     "r02a": None,  # a prebuilt library of commit 8540df6
+    "prev": None,  # a prebuilt library of the previous working state
     "adaptprof": ["TCI_ADAPT_PROFILE=1"],
     "adapt_twice": ["TCI_ADAPT_TWICE=1"],
     "adapt_nochol": ["TCI_ADAPT_ABLATE=1"],

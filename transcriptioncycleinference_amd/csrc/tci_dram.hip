@@ -77,13 +77,13 @@ __device__ __forceinline__ double u01(uint32_t a, uint32_t b) {
 }
 
 // Standard normals of the stream (chain, step, purpose), kNPer per Philox call (item), Box-Muller.
-//   f32 (shipped): two 24-bit uniforms per pair, OCML logf / sincospif (~1 ulp), 4 normals per
-//     call. These are only the proposal DIRECTIONS z (proposal = theta + z*R in FP64): z is N(0,1)
-//     discretised at 2^-24 (tails cut at 5.9 sd), the delayed-rejection ratio uses the same z, so
-//     the sampler stays exact for it; the 299-cell fit runs 6 % faster (A/B).
-//   f64 (TCI_NORMAL_F32=0): two 53-bit uniforms per pair, log / sincospi in FP64, 2 per call.
+//   f64 (shipped): two 53-bit uniforms per pair, log / sincospi in FP64, 2 normals per call: the
+//     double-precision N(0,1) of mcmcstat's randn (no 2^-24 discretisation, no tail cut).
+//   f32 (TCI_NORMAL_F32=1, A/B only): two 24-bit uniforms per pair, OCML logf / sincospif, 4 per
+//     call; z discretised at 2^-24 with the tails cut at 5.9 sd. Measured 5-7 % faster fits
+//     (profiles/r02_likelihood/r02k_dram_libs.jsonl), not worth the narrower proposals.
 #ifndef TCI_NORMAL_F32
-#define TCI_NORMAL_F32 1
+#define TCI_NORMAL_F32 0
 #endif
 constexpr int kNPer = TCI_NORMAL_F32 ? 4 : 2;
 
@@ -894,16 +894,25 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   int64_t nev = st.nevals[c];
   int64_t prow = 0;  // rows prow .. prow + padv - 1 were decided by the previous round (records pending);
   int padv = 0;      // of two, the first did not move the chain (its row is thp)
-  // this wave's proposal offsets: rows s + ahead (cur), s + ahead + 1, s + ahead + 2 (prefetched)
+  // Loads one round ahead. The next round starts at step s + 1 or s + 2, so a round loads both
+  // candidates at its START (this wave's offsets of rows s + ahead + 1 and s + ahead + 2, and the
+  // scalar draws of rows s + 1 .. s + 3) and the next round picks one: a whole round hides the
+  // latency. (Loads issued at the end of the round were waited for at the loop back-edge, where
+  // the rotation of the prefetch registers needs their data: ~2-5 k cycles a round.) The scalar
+  // draws are vector loads (lane j: row r0 + j / 4, slot j % 4) read by readlane: scalar loads
+  // would also be waited for at the evaluation's first LDS wait.
   auto load_u = [&](double* u, int64_t row) {
     const double* src = drow + min(row, s_end) * DW + stage * ld;
 #pragma unroll
     for (int k = 0; k < NJ; ++k) u[k] = lane + 64 * k < P ? src[lane + 64 * k] : 0.0;
   };
+  auto load_sc = [&](int64_t r0) {
+    return lane < 12 ? drow[min(r0 + (lane >> 2), s_end) * DW + 2 * ld + (lane & 3)] : 0.0;
+  };
   double ucur[NJ], un1[NJ], un2[NJ];
   load_u(ucur, s_begin + ahead);
-  load_u(un1, s_begin + ahead + 1);
-  load_u(un2, s_begin + ahead + 2);
+  double dsc = load_sc(s_begin), dscn = 0.0;
+  int sbase = 0;  // lane of step s's first scalar draw in dsc (0 or 4)
   int par = 0;
   RowCursor cur;
   cur.init(p, s_begin);
@@ -933,11 +942,11 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   if (TCI_CHAIN_PROFILE) { t1 = stamp(); ph[k] += t1 - t0; t0 = t1; }
   for (int64_t s = s_begin; s <= s_end; par ^= 1) {
     const bool has_next = s + 1 <= s_end;
-    // the scalar draws of steps s and s+1 (wave-uniform loads)
-    const double* sc0 = drow + s * DW + 2 * ld;
-    const double* sc1 = drow + min(s + 1, s_end) * DW + 2 * ld;
-    const double Q1a = sc0[D_Q1], U1a = sc0[D_U1], U2a = sc0[D_U2], Ga = sc0[D_G];
-    const double Q1b = sc1[D_Q1], U1b = sc1[D_U1], U2b = sc1[D_U2], Gb = sc1[D_G];
+    // the scalar draws of steps s and s+1 (loaded by the previous round)
+    const double Q1a = lane_bcast(dsc, sbase + D_Q1), U1a = lane_bcast(dsc, sbase + D_U1);
+    const double U2a = lane_bcast(dsc, sbase + D_U2), Ga = lane_bcast(dsc, sbase + D_G);
+    const double Q1b = lane_bcast(dsc, sbase + 4 + D_Q1), U1b = lane_bcast(dsc, sbase + 4 + D_U1);
+    const double U2b = lane_bcast(dsc, sbase + 4 + D_U2), Gb = lane_bcast(dsc, sbase + 4 + D_G);
     // ---- this wave's proposal and its bounds (wave vote)
     double y[NJ];
     bool out = false;
@@ -948,6 +957,10 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     }
     const bool active = (stage == 0 || p.ntry >= 2) && (ahead == 0 || has_next);
     const bool inb = active && wave_ballot(out) == 0;
+    // the next round's candidates (see load_u)
+    load_u(un1, s + ahead + 1);
+    load_u(un2, s + ahead + 2);
+    dscn = load_sc(s + 1);
     double r = INFINITY, pr = 0.0;
     TCI_PHASE(0)
     if (inb) {
@@ -1056,20 +1069,11 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     Gl = adv == 1 ? Ga : Gb;
     gpend = p.updatesigma != 0;
     TCI_PHASE(6)
-    // ---- advance the proposal offsets by adv rows
-    if (adv == 1) {
+    // ---- advance by adv rows: the candidates loaded at the start of this round
 #pragma unroll
-      for (int k = 0; k < NJ; ++k) {
-        ucur[k] = un1[k];
-        un1[k] = un2[k];
-      }
-      load_u(un2, s + 1 + ahead + 2);
-    } else {
-#pragma unroll
-      for (int k = 0; k < NJ; ++k) ucur[k] = un2[k];
-      load_u(un1, s + 2 + ahead + 1);
-      load_u(un2, s + 2 + ahead + 2);
-    }
+    for (int k = 0; k < NJ; ++k) ucur[k] = adv == 1 ? un1[k] : un2[k];
+    dsc = dscn;
+    sbase = 4 * (adv - 1);
     s += adv;
     TCI_PHASE(5)
     if (TCI_CHAIN_PROFILE) ph[5] += 1ull << 40;  // round count in the high bits
