@@ -665,11 +665,14 @@ __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
 
 // NWD waves per workgroup: 4 for the FUSED engine (299 TestData chains: 100.6 vs 105.4 ms per 20k
 // steps with 8), 8 for WALK (10,000 chains, one workgroup per CU at P = 207: 175 vs 188 ms per
-// 1000 steps with 4). The wave count only moves column tiles between waves: same bits.
-template <int NWD>
+// 1000 steps with 4). CT column tiles per wave and MFMA call: the smallest CT whose NWD*CT tiles
+// cover the row (draws_ct), since the accumulators of CT*2 tiles set the register count and with
+// it the waves per SIMD; longer rows loop over calls. The wave count and CT only move column
+// tiles between waves and calls: same bits.
+template <int NWD, int CT>
 __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end) {
   constexpr int kDrawWaves = NWD, kDrawThreads = 64 * NWD;
-  constexpr int kDrawCT = (kZrCT * 4 + kDrawWaves - 1) / kDrawWaves;  // column tiles per wave (P <= 320)
+  constexpr int kDrawCT = CT;
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
@@ -1301,11 +1304,20 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
   }
 }
 
+// Column tiles per wave of k_draws: the row's 16-column tiles over the waves, at most 5 (4 waves)
+// or 3 (8 waves) per call.
+inline int draws_ct(int64_t ld, int nwd) {
+  const int64_t tiles = (ld + 15) / 16, per = (tiles + nwd - 1) / nwd;
+  return (int)std::min<int64_t>(per < 2 ? 2 : per, nwd == 8 ? 3 : 5);
+}
+
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    hipStream_t stream) {
   const size_t lds = (size_t)draws_lds_bytes(st.ld);
-  auto kd = p.walk ? k_draws<8> : k_draws<4>;
+  const int ct = draws_ct(st.ld, p.walk ? 8 : 4);
+  auto kd = p.walk ? (ct <= 2 ? k_draws<8, 2> : k_draws<8, 3>)
+                   : (ct <= 2 ? k_draws<4, 2> : ct <= 3 ? k_draws<4, 3> : k_draws<4, 5>);
   if (lds > 48 * 1024 &&
       hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return TCI_EHIP;
