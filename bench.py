@@ -152,17 +152,25 @@ def load_pmc(workload: str) -> dict:
 
 
 def valu_issue(pmc: dict, kernel_ms: float):
-    """The bound that actually limits this FP64 kernel: VALU issue. A wave64 VALU instruction
-    occupies its SIMD (16 lanes) for 4 cycles; FP64 FMA runs at that full rate on gfx950
-    (78.6 TF/s = 1024 SIMDs x 16 lanes x 2 x 2.4 GHz). Peak = 1024 x 2.4e9 / 4 wave-instructions/s.
-    achieved = SQ_INSTS_VALU per launch (committed PMC pass) / the live per-launch kernel time."""
-    insts = (pmc.get("counters_mean_per_launch") or {}).get("SQ_INSTS_VALU")
+    """VALU issue utilisation of the FP64 kernel from the committed PMC passes, priced per class:
+    a wave64 FP64 instruction (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64) holds its SIMD for 4 cycles
+    (78.6 TF/s FP64 = 1024 SIMDs x 16 lanes x 2 x 2.4 GHz), a 32-bit one for 2 (SIMD-32). The
+    instructions in no class (moves, DPP moves, compares, selects, min/max) are priced at 2 cycles
+    for `frac` and at 4 for `frac_high`. busy = issue cycles / (1024 SIMDs x 2.4 GHz x launch time)."""
+    cnt = pmc.get("counters_mean_per_launch") or {}
+    insts = cnt.get("SQ_INSTS_VALU")
     if not insts or kernel_ms <= 0:
         return None
-    peak = SIMDS * CLOCK_HZ / 4.0
-    achieved = insts / (kernel_ms * 1e-3)
-    return {"achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "G VALU wave-instr/s", "frac": achieved / peak,
-            "valu_insts_per_launch": insts, "source": pmc.get("source")}
+    fp64 = sum(cnt.get(f"SQ_INSTS_VALU_{k}_F64", 0.0) for k in ("ADD", "MUL", "FMA", "TRANS"))
+    avail = SIMDS * CLOCK_HZ * kernel_ms * 1e-3
+    out = {"valu_insts_per_launch": insts, "fp64_insts_per_launch": fp64 or None, "source": pmc.get("source"),
+           "unit": "fraction of SIMD issue cycles"}
+    if fp64:
+        lo, hi = 4.0 * fp64 + 2.0 * (insts - fp64), 4.0 * insts
+        out.update({"frac": lo / avail, "frac_high": hi / avail, "issue_cycles_per_launch": [lo, hi]})
+    else:
+        out.update({"frac_high": 4.0 * insts / avail})
+    return out
 
 
 def _cpu_rate(cells, cs, th, ci, ac, threads: int, seconds: float):
@@ -540,8 +548,8 @@ def main():
             "traffic": traffic,
             "kernel_ms": kernel_ms,
             "algorithmic_bytes_per_launch": alg,
-            "note": "VALU-issue/latency-bound FP64 path (see 'valu'); HBM fraction reported as the north star asks "
-                    "(DESIGN.md §3)",
+            "note": "FP64 path bound by each wave's dependent chain under issue contention, no unit saturated "
+                    "(see 'valu'; DESIGN.md §3); HBM fraction reported as the north star asks",
             "valu": valu_issue(pmc, kernel_ms),
         },
         "results_finite": finite_ok,

@@ -21,7 +21,7 @@ rc=$?; cat "$OUT/${TAG}_bench.json"; stop_if_fault $rc
 echo "== rocprofv3 kernel trace"
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof" -o trace -- \
-  python3 "$ROOT/bench.py" --no-cpu-baseline --dram-steps 0 --no-configs > "$OUT/${TAG}_prof_bench.json" 2> "$OUT/${TAG}_prof.err"
+  python3 "$ROOT/bench.py" --no-cpu-baseline --dram-steps 0 --no-configs --no-sweep --no-latency > "$OUT/${TAG}_prof_bench.json" 2> "$OUT/${TAG}_prof.err"
 rc=$?; stop_if_fault $rc
 find "$OUT/${TAG}_prof" -name "*stats*" | head -5
 exit 0

@@ -15,7 +15,7 @@ import sys
 
 def main(prefix, workload):
     agg = collections.defaultdict(list)
-    for p in range(1, 5):
+    for p in range(1, 7):
         try:
             rows = list(csv.DictReader(open(f"{prefix}_p{p}/pmc_counter_collection.csv")))
         except OSError:

@@ -22,7 +22,8 @@ def rel_err(a, b):
     both_nan = np.isnan(a) & np.isnan(b)
     both_inf = np.isinf(a) & np.isinf(b) & (np.sign(a) == np.sign(b))
     ok = both_nan | both_inf
-    d = np.where(ok, 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
+    with np.errstate(invalid="ignore"):
+        d = np.where(ok, 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-300))
     d[np.isnan(d)] = np.inf
     return float(np.max(d)) if d.size else 0.0
 
@@ -208,6 +209,41 @@ def test_edge_cases_vs_oracle(lk, cells, construct, c_oracle):
     ss = lk.ss_batch(theta, cid)
     want = oracle_ss(c_oracle, cells, construct, theta, cid)
     assert rel_err(ss, want) <= REL
+
+
+def test_positions_on_a_threshold_take_the_exact_sweep(lk, cells, construct, c_oracle):
+    """Rates v that put a representative position P_m = m*(v*d) onto a decision threshold (a loop
+    start or end, or the gene end L = L0 + tau*v): the lane-parallel distance cut (tci_eval.h,
+    distance_cut) must flag the ambiguity, the wave takes the exact sweep, and the SS equals the
+    oracle's -- and the forced exact sweep's -- for every such row."""
+    rows, cid = [], []
+    a_m, e_m, a_p, e_p, L0 = 0.024, 1.299, 4.292, 5.758, 6.626  # P2P-MS2v5-LacZ-PP7v4 (GetFluorFromPolPos.m:18-28)
+    for c in (0, 7, 42, 123, 298):
+        t = cells.cell(c)[0]
+        n = len(t)
+        d = float(np.sum(np.diff(t))) / (n - 1)  # the grid increment (SumofSquares...m:29)
+        for m in (1, 3, 10, 25):
+            if m >= n - 1:
+                continue
+            tau = 2.0
+            for v in (a_m / (m * d), e_m / (m * d), a_p / (m * d), e_p / (m * d), L0 / (m * d - tau)):
+                if not (0.0 < v < 20.0):
+                    continue
+                r = np.concatenate([[v, tau, t[0] + 0.5, 1.0, 2.0, 0.7, 9.0], np.zeros(n)])
+                rows.append(r)
+                cid.append(c)
+    theta = pack(rows)
+    cid = np.array(cid, np.int32)
+    ss = lk.ss_batch(theta, cid)
+    want = oracle_ss(c_oracle, cells, construct, theta, cid)
+    assert rel_err(ss, want) <= REL
+    lk.set_force_exact(positions=True)
+    try:
+        ex = lk.ss_batch(theta, cid)
+    finally:
+        lk.set_force_exact()
+    assert rel_err(ss, ex) <= REL
+    print(f"{len(ss)} rows with a position on a threshold, max rel err vs oracle {rel_err(ss, want):.2e}")
 
 
 def test_inactive_rows_and_nonfinite_theta(lk, cells, chain):

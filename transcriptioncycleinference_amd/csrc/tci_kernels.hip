@@ -52,18 +52,10 @@ __global__ __launch_bounds__(64 * TCI_WAVES_PER_BLOCK) TCI_OCCUPANCY void tci_co
   return;
 #endif
 
-  // ---- round trip 1: what the row index alone addresses -- the cell id, the active flag and the
-  //      wave-uniform theta entries (ld >= 9 is checked by the host, so th[0..6] is inside the row)
+  // ---- the row's cell id and active flag, then every other load of the evaluation at once. (Also
+  //      reading the theta scalars with the cell id, one round trip earlier, measured no faster and
+  //      fetched the theta lines of the bounds-rejected rows too: DESIGN.md §3.)
   const int c = __builtin_amdgcn_readfirstlane(cell_id[b]);
-  const double* th = theta + b * ld;
-  EvalIn<RPL> e;
-  e.v = th[0];
-  e.tau = th[1];
-  e.ton = th[2];
-  e.b1 = th[3];
-  e.b2 = th[4];
-  e.A = th[5];
-  e.R = th[6];
   const bool act = MODE != MODE_SS || active == nullptr || active[b] != 0;
   if (!act) {
     if (lane == 0) out0[b] = INFINITY;  // skipped proposal (bounds-rejected by the caller)
@@ -73,24 +65,28 @@ __global__ __launch_bounds__(64 * TCI_WAVES_PER_BLOCK) TCI_OCCUPANCY void tci_co
     write_nan<MODE>(lane, 0, b, out0, out1, ld_out);
     return;
   }
-  // ---- round trip 2: the cell's records and the row's dR entries
+  const double* th = theta + b * ld;
+  EvalIn<RPL> e;
   load_cell<RPL, MODE == MODE_FWD_RAW>(kp, c, lane, e);
+  e.v = th[0];
+  e.tau = th[1];
+  e.ton = th[2];
+  e.b1 = th[3];
+  e.b2 = th[4];
+  e.A = th[5];
+  e.R = th[6];
 #pragma unroll
   for (int q = 0; q < RPL; ++q) {
     const int g = RPL * lane + q;
     e.dr[q] = 7 + g < ld ? th[7 + g] : 0.0;  // speculative (N unknown yet), kept inside the row
   }
   const int N = e.cm.n;
-  // A row shorter than 7 + N gives NaN. SS mode decides that after the evaluation (the dR loads
-  // above stay inside the row either way): a branch on N here would hold back the theta loads
-  // until the cell record has arrived, one more round trip.
-  const bool short_row = ld < 7 + N;
-  if (MODE != MODE_SS && short_row) {
+  if (ld < 7 + N) {  // a row shorter than 7 + N entries
     write_nan<MODE>(lane, N, b, out0, out1, ld_out);
     return;
   }
   const double ss = eval_wave<RPL, NSEG, MODE>(kp, e, lane, lds, b, out0, out1, ld_out);
-  if (MODE == MODE_SS && lane == 0) out0[b] = short_row ? NAN : ss;
+  if (MODE == MODE_SS && lane == 0) out0[b] = ss;
 }
 
 template <int RPL, int NSEG, int MODE>
