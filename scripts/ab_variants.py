@@ -51,6 +51,8 @@ VARIANTS = {
     "draws_p4": ["TCI_DRAW_PASSES=4"],
     "draws_p7": ["TCI_DRAW_PASSES=7"],
     "draws_p1": ["TCI_DRAW_PASSES=1"],
+    "launder0": ["TCI_LOOP_LAUNDER=0"],
+    "launder1": ["TCI_LOOP_LAUNDER=1"],
 }
 
 

@@ -828,6 +828,14 @@ __device__ __forceinline__ uint64_t stamp() {
 #define TCI_SIG_WAVE 2
 #endif
 constexpr int kRecWave = TCI_REC_WAVE, kSigWave = TCI_SIG_WAVE;
+// k_chain / k_walk loop heads: the lane index is re-laundered every round/step, so the 64-bit lane
+// masks derived from it are recomputed (one compare each) instead of living in scalar pairs
+// across the loop. Register allocation only (same bits): it removes k_walk's VGPR spill at RPL = 4
+// (config 5: 199.7 -> 191-193 us per step) and trims the SGPR spill (k_chain<2,1>: 171 -> 126
+// dwords, which measured no faster: the reloads are off the critical path). 0 = off (A/B).
+#ifndef TCI_LOOP_LAUNDER
+#define TCI_LOOP_LAUNDER 1
+#endif
 
 template <int RPL, int NSEG>
 __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
@@ -857,7 +865,8 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   __shared__ double xip[2][2];                                  // by round parity: the precisions of steps s, s+1
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;  // re-laundered every round (TCI_LOOP_LAUNDER)
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int64_t DW = draw_stride(ld);
@@ -944,12 +953,12 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 #define TCI_PHASE(k) \
   if (TCI_CHAIN_PROFILE) { t1 = stamp(); ph[k] += t1 - t0; t0 = t1; }
   for (int64_t s = s_begin; s <= s_end; par ^= 1) {
+#if TCI_LOOP_LAUNDER
+    asm volatile("" : "+v"(lane));
+#endif
     const bool has_next = s + 1 <= s_end;
-    // the scalar draws of steps s and s+1 (loaded by the previous round)
-    const double Q1a = lane_bcast(dsc, sbase + D_Q1), U1a = lane_bcast(dsc, sbase + D_U1);
-    const double U2a = lane_bcast(dsc, sbase + D_U2), Ga = lane_bcast(dsc, sbase + D_G);
-    const double Q1b = lane_bcast(dsc, sbase + 4 + D_Q1), U1b = lane_bcast(dsc, sbase + 4 + D_U1);
-    const double U2b = lane_bcast(dsc, sbase + 4 + D_U2), Gb = lane_bcast(dsc, sbase + 4 + D_G);
+    // the scalar draws of steps s and s+1 (loaded by the previous round; dsc lane sbase + 4 h + slot)
+    // are broadcast where they are used, so no scalar copy lives across the evaluation
     // ---- this wave's proposal and its bounds (wave vote)
     double y[NJ];
     bool out = false;
@@ -996,6 +1005,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       // lanes 0-2: s2 of the last decided row (pending: 1/(Gl*(2/ss))), after step s unmoved
       // (1/(G_s*(2/ss))), after step s+1 with step s unmoved (1/(G_s+1*(2/ss))); lanes 0-1 also
       // the precision of that s2, which the decisions of steps s and s+1 use
+      const double Ga = lane_bcast(dsc, sbase + D_G), Gb = lane_bcast(dsc, sbase + 4 + D_G);
       const double gv = lane == 0 ? Gl : lane == 1 ? Ga : Gb;
       double x = 1.0 / (gv * (2.0 / ss));
       if (!p.updatesigma || (lane == 0 && !gpend)) x = s2c;
@@ -1037,6 +1047,10 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     const double a12a = lane_bcast(av, 0), a32a = lane_bcast(av, 1), l2a = lane_bcast(av, 2);
     const double a12b = lane_bcast(av, 3), a32b = lane_bcast(av, 4), l2b = lane_bcast(av, 5);
     TCI_PHASE(4)
+    const double Q1a = lane_bcast(dsc, sbase + D_Q1), U1a = lane_bcast(dsc, sbase + D_U1);
+    const double U2a = lane_bcast(dsc, sbase + D_U2);
+    const double Q1b = lane_bcast(dsc, sbase + 4 + D_Q1), U1b = lane_bcast(dsc, sbase + 4 + D_U1);
+    const double U2b = lane_bcast(dsc, sbase + 4 + D_U2);
     int adv = 0;
     for (int hh = 0; hh < 2; ++hh) {
       if (hh == 1 && !has_next) break;
@@ -1069,7 +1083,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     // the rows s .. s + adv - 1 are recorded next round (s2 of the last: 1/(G*(2/ss)), ss after it)
     prow = s;
     padv = adv;
-    Gl = adv == 1 ? Ga : Gb;
+    Gl = lane_bcast(dsc, sbase + 4 * (adv - 1) + D_G);
     gpend = p.updatesigma != 0;
     TCI_PHASE(6)
     // ---- advance by adv rows: the candidates loaded at the start of this round
@@ -1147,7 +1161,8 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
   __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each wave's {K,J} tables / rows
   __shared__ double yl[NW][64 * NJ];                            // each wave's proposal (theta broadcast)
   __shared__ double rec[NW][3][64 * NJ];                        // posterior Welford mean / M2, window sums
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int lane = threadIdx.x & 63;  // re-laundered every step (TCI_LOOP_LAUNDER)
   const int64_t c = (int64_t)blockIdx.x * NW + w;
   if (c >= st.n_chains) return;  // uniform per wave; no workgroup barriers below
   const int64_t ld = st.ld;
@@ -1239,6 +1254,9 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
     for (int k = 0; k < NJ; ++k) u[k] = lane + 64 * k < P ? src[lane + 64 * k] : 0.0;
   };
   for (int64_t s = s_begin; s <= s_end; ++s) {
+#if TCI_LOOP_LAUNDER
+    asm volatile("" : "+v"(lane));
+#endif
     double u[NJ];
     load_u(u, s, 0);
     const double* sc = drow + s * DW + 2 * ld;
