@@ -53,6 +53,14 @@ VARIANTS = {
     "draws_p1": ["TCI_DRAW_PASSES=1"],
     "launder0": ["TCI_LOOP_LAUNDER=0"],
     "launder1": ["TCI_LOOP_LAUNDER=1"],
+    "drawsflat": ["TCI_DRAWS_FLAT=1"],
+    "gt1": ["TCI_GT_BATCH=1"],
+    "gt4": ["TCI_GT_BATCH=4"],
+    "gtper1": ["TCI_GT_PER=1"],
+    "gtper4": ["TCI_GT_PER=4"],
+    "gtmg2": ["TCI_GT_MG=2"],
+    "grp2": ["TCI_DRAW_PASSES_GR=2"],
+    "grp7": ["TCI_DRAW_PASSES_GR=7"],
 }
 
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Bitwise comparison of two library builds on the same DRAM fit (A/B of a change that must not
 move any bit): python scripts/dram_lib_equal.py LIB_A LIB_B [STEPS] [CELLS] [CFG]
-("main" = the in-tree build). CFG 0: TestData cells; 4/5: BASELINE config-4/5 synthetic cells."""
+("main" = the in-tree build). CFG 0: TestData cells; 4/5: BASELINE config-4/5 synthetic cells
+(TCI_SYNTH_POINTS points per cell, default 200)."""
 import json
 import os
 import sys
@@ -19,7 +20,7 @@ def run(lib, steps, n, cfg):
         cells, con = testdata(), "P2P-MS2v5-LacZ-PP7v4"
     else:
         import bench
-        cells, _, con = bench.synthetic_config_cells(cfg, 0, 1, 0)[:3]
+        cells, _, con = bench.synthetic_config_cells(cfg, 0, 1, 0, int(os.environ.get("TCI_SYNTH_POINTS", "200")))[:3]
     with Likelihood(cells, con, lib_path=path) as lk:
         fr = fit(lk, n_steps=steps, n_burn=steps // 4, seed=3, cells=list(range(n)))
     return np.array([[r[k] for k in sorted(r) if np.isscalar(r[k]) and isinstance(r[k], float)] for r in fr.MCMCresults])

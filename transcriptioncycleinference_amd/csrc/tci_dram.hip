@@ -380,9 +380,11 @@ __device__ bool propose_block(const DramState& st, const DramParams& p, int64_t 
   __syncthreads();
   double* U = sm.y;
   const int us = sm.L;
-  const float* Rsrc = rl ? sm.Rl : st.Rf + c * tri_stride(st.ld);
-  for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= 4 * kZrCT)
-    mfma_zr<1, kZrCT, 4>(sm.z, sm.L, 1, Rsrc, P, top, [=](int r, int j, double v) { U[r * us + j] = v; });
+  const auto put = [=](int r, int j, double v) { U[r * us + j] = v; };
+  for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= 4 * kZrCT) {
+    if (rl) mfma_zr<1, kZrCT, 4>(sm.z, sm.L, 1, sm.Rl, P, top, put);  // two calls: each one's R pointer has
+    else mfma_zr<1, kZrCT, 4>(sm.z, sm.L, 1, st.Rf + c * tri_stride(st.ld), P, top, put);  // a known address space
+  }
   __syncthreads();
   int inb = 1;
   for (int j = threadIdx.x; j < P; j += kThreads) {
@@ -641,6 +643,9 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
   }
 }
 
+#ifndef TCI_DRAWS_FLAT
+#define TCI_DRAWS_FLAT 0  // A/B only: 1 = one z*R call through a selected (generic) R pointer
+#endif
 #ifndef TCI_DRAWS_ABLATE
 #define TCI_DRAWS_ABLATE 0  // diagnostics only (wrong results): bit0 no normals, bit1 no MFMA, bit2 no scalars, bit3 no R load
 #endif
@@ -650,6 +655,12 @@ constexpr int kDrawSteps = 8 * kDrawMT;   // steps per pass (2 rows per step)
 #define TCI_DRAW_PASSES 2
 #endif
 constexpr int kDrawPasses = TCI_DRAW_PASSES;  // passes per k_draws workgroup (32 steps)
+#ifndef TCI_DRAW_PASSES_GR
+#define TCI_DRAW_PASSES_GR 4
+#endif
+// passes per workgroup when R is read from global memory (past the LDS budget): every workgroup
+// reads the chain's whole R once per pass, so fewer, longer workgroups read it fewer times
+constexpr int kDrawPassesGR = TCI_DRAW_PASSES_GR;
 enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
 
 // Dynamic LDS of k_draws: one pass's normals (2 x kDrawSteps rows of stride L) and the chain's R
@@ -662,6 +673,7 @@ __host__ __device__ inline bool draws_r_lds(int64_t L) {
 __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
   return (2 * kDrawSteps * L) * 8 + (draws_r_lds(L) ? (L * (L + 1) / 2) * 4 : 0) + 16;
 }
+__host__ __device__ inline int draws_passes(int64_t ld) { return draws_r_lds(ld) ? kDrawPasses : kDrawPassesGR; }
 
 // NWD waves per workgroup: 4 for the FUSED engine (299 TestData chains: 100.6 vs 105.4 ms per 20k
 // steps with 8), 8 for WALK (10,000 chains, one workgroup per CU at P = 207: 175 vs 188 ms per
@@ -670,7 +682,7 @@ __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
 // it the waves per SIMD; longer rows loop over calls. The wave count and CT only move column
 // tiles between waves and calls: same bits.
 template <int NWD, int CT>
-__global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end) {
+__global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end, int npass) {
   constexpr int kDrawWaves = NWD, kDrawThreads = 64 * NWD;
   constexpr int kDrawCT = CT;
   extern __shared__ __attribute__((aligned(16))) double dyn[];
@@ -686,22 +698,31 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
   float* Rl = reinterpret_cast<float*>(Z + 2 * kDrawSteps * L);
   const bool rl = draws_r_lds(ld);
   if (rl && !(TCI_DRAWS_ABLATE & 8)) load_R_f32<kDrawThreads>(Rl, st, c, P);
-  const float* Rsrc = rl ? Rl : st.Rf + c * tri_stride(ld);
+  const float* Rg = st.Rf + c * tri_stride(ld);
   const double a = 0.5 * (double)st.nobs[c];
   const double inv_ds = 1.0 / p.drscale;
   double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
-  for (int pass = 0; pass < kDrawPasses; ++pass) {
-    const int64_t step0 = s_begin + ((int64_t)blockIdx.y * kDrawPasses + pass) * kDrawSteps;
+  for (int pass = 0; pass < npass; ++pass) {
+    const int64_t step0 = s_begin + ((int64_t)blockIdx.y * npass + pass) * kDrawSteps;
     if (step0 > s_end) break;  // uniform over the workgroup
     const int ns = (int)min<int64_t>(kDrawSteps, s_end - step0 + 1);
     if (!(TCI_DRAWS_ABLATE & 1)) draw_block_normals<kDrawThreads>(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
     __syncthreads();  // (the first pass: also R)
     // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
     double* d0 = drow + step0 * DW;
+    // R from LDS or global memory: two call sites, so that each inlined copy reads R with the
+    // instructions of its address space (one call through a selected pointer made every R read a
+    // flat load, with global-memory latency, also from LDS)
+    const auto put = [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; };
     if (!(TCI_DRAWS_ABLATE & 2))
-      for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT)
-        mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rsrc, P, top,
-                                              [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; });
+      for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT) {
+#if TCI_DRAWS_FLAT
+        mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, rl ? (const float*)Rl : Rg, P, top, put);
+#else
+        if (rl) mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rl, P, top, put);
+        else mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rg, P, top, put);
+#endif
+      }
     for (int k = w; k < ns; k += kDrawWaves) {
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
       if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
@@ -709,8 +730,8 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
     __syncthreads();  // Z is rewritten by the next pass
   }
   // the scalar draws of the workgroup's steps, one step per thread
-  const int64_t step = s_begin + (int64_t)blockIdx.y * kDrawPasses * kDrawSteps + threadIdx.x;
-  if (!(TCI_DRAWS_ABLATE & 4) && threadIdx.x < kDrawPasses * kDrawSteps && step <= s_end) {
+  const int64_t step = s_begin + (int64_t)blockIdx.y * npass * kDrawSteps + threadIdx.x;
+  if (!(TCI_DRAWS_ABLATE & 4) && threadIdx.x < npass * kDrawSteps && step <= s_end) {
     double* sc = drow + step * DW + 2 * ld;
     sc[D_U1] = uniform_at(p.seed, key, step, P_U1);
     sc[D_U2] = uniform_at(p.seed, key, step, P_U2);
@@ -1339,9 +1360,11 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
   if (lds > 48 * 1024 &&
       hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return TCI_EHIP;
-  const int64_t per_wg = (int64_t)kDrawSteps * kDrawPasses;
+  const int npass = draws_passes(st.ld);
+  const int64_t per_wg = (int64_t)kDrawSteps * npass;  // <= the workgroup's threads (scalar draws)
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
-  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(p.walk ? 512 : 256), lds, stream, st, p, s_begin, s_end);
+  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(p.walk ? 512 : 256), lds, stream, st, p, s_begin, s_end,
+                     npass);
   if (p.walk)
     hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, stream, st, p,
                        kp, s_begin, s_end);
@@ -1716,7 +1739,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8
 //     was positive (a singular matrix keeps the previous R, as mcmcstat).
 // The tile arithmetic is k_adapt_mfma's, so both kernels give the same R up to the order of the
 // scatter's k-steps (rows in batches here).
-constexpr int kGtWaves = 8, kGtTiles = 8;
+#ifndef TCI_GT_TILES
+#define TCI_GT_TILES 8
+#endif
+constexpr int kGtWaves = 8, kGtTiles = TCI_GT_TILES;
+#ifndef TCI_GT_BATCH
+#define TCI_GT_BATCH 2
+#endif
+constexpr int kGtBatch = TCI_GT_BATCH;  // trailing / R-store tiles whose loads are issued together
+#ifndef TCI_GT_PER
+#define TCI_GT_PER 8
+#endif
+constexpr int kGtPer = TCI_GT_PER;  // window loads in flight per thread
+#ifndef TCI_GT_MG
+#define TCI_GT_MG 1
+#endif
+constexpr int kGtMG = TCI_GT_MG;  // merge group: tiles whose old covariance values are read together
 __host__ __device__ inline int64_t gt_lt(int64_t ld) { return (ld + 15) / 16 * 16; }  // tile-grid side
 __host__ __device__ inline int gt_rows(int64_t P) {  // window rows per LDS batch
   const int64_t LX = (P + 15) / 16 * 16;
@@ -1788,9 +1826,20 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
     for (int r0 = 0; r0 < nb; r0 += rb) {
       const int n = min(rb, nb - r0);
       __syncthreads();  // the previous batch is consumed (and mb is written, first time)
-      for (int e = t; e < rb * LX; e += NTH) {
-        const int r = e / LX, j = e - r * LX;
-        X[e] = (r < n && j < P) ? win[(int64_t)(r0 + r) * ld + j] - mb[j] : 0.0;
+      // the batch's window entries, kGtPer loads in flight per thread before their LDS stores (a
+      // plain strided loop waited for each load in turn)
+      for (int e0 = t; e0 < rb * LX; e0 += kGtPer * NTH) {
+        double v[kGtPer];
+#pragma unroll
+        for (int u = 0; u < kGtPer; ++u) {
+          const int e = e0 + u * NTH, r = e / LX, j = e - r * LX;
+          v[u] = (e < rb * LX && r < n && j < P) ? win[(int64_t)(r0 + r) * ld + j] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kGtPer; ++u) {
+          const int e = e0 + u * NTH, r = e / LX, j = e - r * LX;
+          if (e < rb * LX) X[e] = (r < n && j < P) ? v[u] - mb[j] : 0.0;
+        }
       }
       __syncthreads();
       for (int k0 = 0; k0 < n; k0 += 4) {
@@ -1801,14 +1850,22 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
       }
     }
 #pragma unroll
-    for (int g = 0; g < kGtTiles; ++g) {
-      if (!val[g]) continue;  // uniform
-      double old[4];
+    for (int g0 = 0; g0 < kGtTiles; g0 += kGtMG) {
+      // every old value of a group of tiles before any write (a diagonal tile reads the mirrors of
+      // its own elements; one round trip per group)
+      double oldg[kGtMG][4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {  // every old value of the tile before any write (mirrors)
-        const int i = 16 * ti[g] + kq + 4 * q, j = 16 * tj[g] + row;
-        old[q] = (i < P && j < P && na > 0.0) ? cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i] : 0.0;
-      }
+      for (int h = 0; h < kGtMG; ++h)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int g = g0 + h, i = 16 * ti[g] + kq + 4 * q, j = 16 * tj[g] + row;
+          oldg[h][q] = (val[g] && i < P && j < P && na > 0.0) ? cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i] : 0.0;
+        }
+#pragma unroll
+    for (int h = 0; h < kGtMG; ++h) {
+      const int g = g0 + h;
+      if (!val[g]) continue;  // uniform
+      const double* old = oldg[h];
       double* A = tile(ti[g], tj[g]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1831,6 +1888,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
         }
         A[(kq + 4 * q) * 16 + row] = a;
       }
+    }
     }
   }
   __syncthreads();  // mb / mo reads, tile writes
@@ -1900,36 +1958,64 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
       }
     }
     __syncthreads();
-    {  // (3) trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj (4 MFMAs), round-robin over waves
+    {  // (3) trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj (4 MFMAs), round-robin over
+       // waves, kGtBatch tiles at a time: every load of the batch is issued before the first store
+       // (one memory round trip per batch, not per tile: the stores may alias later loads)
       const int m = NT - pk - 1, Ttr = m * (m + 1) / 2;
-      for (int k = w; k < Ttr; k += NW) {
-        int ti, tj;
-        tri_tile(k, m, pk + 1, ti, tj);
-        double* A = tile(ti, tj);
-        const double* Xi = tile(pk, ti);
-        const double* Xj = tile(pk, tj);
-        f64x4 acc;
+      for (int k0 = w; k0 < Ttr; k0 += NW * kGtBatch) {
+        double* Ap[kGtBatch];
+        f64x4 acc[kGtBatch];
+        double xi[kGtBatch][4], xj[kGtBatch][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = A[(kq + 4 * q) * 16 + row];
+        for (int g = 0; g < kGtBatch; ++g) {
+          const int k = k0 + g * NW;
+          if (k >= Ttr) break;  // uniform
+          int ti, tj;
+          tri_tile(k, m, pk + 1, ti, tj);
+          Ap[g] = tile(ti, tj);
+          const double* Xi = tile(pk, ti);
+          const double* Xj = tile(pk, tj);
 #pragma unroll
-        for (int k4 = 0; k4 < 16; k4 += 4)
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Xi[(k4 + kq) * 16 + row], Xj[(k4 + kq) * 16 + row], acc, 0, 0, 0);
+          for (int q = 0; q < 4; ++q) {
+            acc[g][q] = Ap[g][(kq + 4 * q) * 16 + row];
+            xi[g][q] = Xi[(4 * q + kq) * 16 + row];
+            xj[g][q] = Xj[(4 * q + kq) * 16 + row];
+          }
+        }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) A[(kq + 4 * q) * 16 + row] = acc[q];
+        for (int g = 0; g < kGtBatch; ++g) {
+          if (k0 + g * NW >= Ttr) break;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(-xi[g][q], xj[g][q], acc[g], 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Ap[g][(kq + 4 * q) * 16 + row] = acc[g][q];
+        }
       }
     }
     __syncthreads();
   }
   if (ok) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
-    for (int k = w; k < T; k += NW) {
-      int ti, tj;
-      tri_tile(k, NT, 0, ti, tj);
-      const double* A = tile(ti, tj);
+    for (int k0 = w; k0 < T; k0 += NW * kGtBatch) {  // batches of loads, as in (3)
+      double a[kGtBatch][4];
+      int tis[kGtBatch], tjs[kGtBatch];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = 16 * ti + kq + 4 * q, j = 16 * tj + row;
-        if (i < P && j < P && j >= i) store_R(st, c, P, i, j, f32_round(A[(kq + 4 * q) * 16 + row] * sc));
+      for (int g = 0; g < kGtBatch; ++g) {
+        const int k = k0 + g * NW;
+        if (k >= T) break;  // uniform
+        tri_tile(k, NT, 0, tis[g], tjs[g]);
+        const double* A = tile(tis[g], tjs[g]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[g][q] = A[(kq + 4 * q) * 16 + row];
+      }
+#pragma unroll
+      for (int g = 0; g < kGtBatch; ++g) {
+        if (k0 + g * NW >= T) break;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = 16 * tis[g] + kq + 4 * q, j = 16 * tjs[g] + row;
+          if (i < P && j < P && j >= i) store_R(st, c, P, i, j, f32_round(a[g][q] * sc));
+        }
       }
     }
   }
