@@ -61,6 +61,7 @@ VARIANTS = {
     "gtmg2": ["TCI_GT_MG=2"],
     "grp2": ["TCI_DRAW_PASSES_GR=2"],
     "grp7": ["TCI_DRAW_PASSES_GR=7"],
+    "glds0": ["TCI_DRAWS_GLDS=0"],
 }
 
 

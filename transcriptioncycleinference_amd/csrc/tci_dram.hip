@@ -235,10 +235,23 @@ __device__ __forceinline__ double f32_round(double x) { return (double)(float)x;
 // global memory (chain c at c * tri_stride(ld)), written beside every write of R (store_R), so a
 // workgroup stages it into LDS with one coalesced copy.
 __device__ __forceinline__ int tri_off(int i, int P) { return i * P - (i * (i - 1)) / 2; }
-__host__ __device__ inline int64_t tri_stride(int64_t ld) { return ld * (ld + 1) / 2; }
+__host__ __device__ inline int64_t tri_stride(int64_t ld) { return dram_tri_stride(ld); }
 __device__ __forceinline__ void store_R(const DramState& st, int64_t c, int P, int i, int j, double v) {
   st.R[c * st.ld * st.ld + (int64_t)i * st.ld + j] = v;
   if (j >= i) st.Rf[c * tri_stride(st.ld) + tri_off(i, P) + j - i] = (float)v;
+}
+// The same copy by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction, no registers):
+// every piece is in flight at once, and the caller's next work (the draws pass's normals) runs
+// while they land; the caller's __syncthreads waits for them. Rl: 16-byte aligned, room for the
+// triangle rounded up to 256 floats (the source stride is, dram_tri_stride).
+template <int NTH>
+__device__ __forceinline__ void load_R_glds(float* Rl, const DramState& st, int64_t c, int P) {
+  const float* src = st.Rf + c * tri_stride(st.ld);
+  const int pieces = (P * (P + 1) / 2 + 255) >> 8;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  for (int k = w; k < pieces; k += NTH / 64)
+    __builtin_amdgcn_global_load_lds((const void*)(src + 256 * k + 4 * lane),
+                                     (__attribute__((address_space(3))) void*)(Rl + 256 * k), 16, 0, 0);
 }
 template <int NTH = kThreads>
 __device__ void load_R_f32(float* Rl, const DramState& st, int64_t c, int P) {
@@ -643,6 +656,9 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
   }
 }
 
+#ifndef TCI_DRAWS_GLDS
+#define TCI_DRAWS_GLDS 1  // stage R by LDS-DMA (load_R_glds); 0 = through registers (A/B)
+#endif
 #ifndef TCI_DRAWS_FLAT
 #define TCI_DRAWS_FLAT 0  // A/B only: 1 = one z*R call through a selected (generic) R pointer
 #endif
@@ -668,10 +684,10 @@ enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a d
 // R is staged only while it fits beside the normals; longer rows read the packed fp32 R from global
 // memory in the same MFMA order (the same bits).
 __host__ __device__ inline bool draws_r_lds(int64_t L) {
-  return (2 * kDrawSteps * L) * 8 + (L * (L + 1) / 2) * 4 + 16 <= 160 * 1024;
+  return (2 * kDrawSteps * L) * 8 + dram_tri_stride(L) * 4 + 16 <= 160 * 1024;
 }
 __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
-  return (2 * kDrawSteps * L) * 8 + (draws_r_lds(L) ? (L * (L + 1) / 2) * 4 : 0) + 16;
+  return (2 * kDrawSteps * L) * 8 + (draws_r_lds(L) ? dram_tri_stride(L) * 4 : 0) + 16;
 }
 __host__ __device__ inline int draws_passes(int64_t ld) { return draws_r_lds(ld) ? kDrawPasses : kDrawPassesGR; }
 
@@ -697,7 +713,11 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
   double* Z = dyn;
   float* Rl = reinterpret_cast<float*>(Z + 2 * kDrawSteps * L);
   const bool rl = draws_r_lds(ld);
+#if TCI_DRAWS_GLDS
+  if (rl && !(TCI_DRAWS_ABLATE & 8)) load_R_glds<kDrawThreads>(Rl, st, c, P);
+#else
   if (rl && !(TCI_DRAWS_ABLATE & 8)) load_R_f32<kDrawThreads>(Rl, st, c, P);
+#endif
   const float* Rg = st.Rf + c * tri_stride(ld);
   const double a = 0.5 * (double)st.nobs[c];
   const double inv_ds = 1.0 / p.drscale;
@@ -1803,6 +1823,11 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
   auto tile = [&](int ti, int tj) { return Wt + ((int64_t)ti * NT + tj) * 256; };
   const int nb = (int)p.adaptint;
   const double* win = st.window + c * p.adaptint * ld;
+  // TCI_ADAPT_PROFILE: thread 0's s_memtime cycles per phase: scatter, merge, diagonal tiles,
+  // panel solves, trailing updates, R store
+  uint64_t aph[6] = {0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
+#define TCI_GPHASE(k) \
+  if (TCI_ADAPT_PROFILE) { a1 = stamp(); aph[k] += a1 - a0; a0 = a1; }
   for (int j = t; j < LX; j += NTH) {
     mb[j] = j < P ? st.wsumv[c * ld + j] / (double)p.adaptint : 0.0;
     mo[j] = j < P ? mu[j] : 0.0;
@@ -1849,6 +1874,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
           if (val[g]) acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr[16 * ti[g]], xr[16 * tj[g]], acc[g], 0, 0, 0);
       }
     }
+    TCI_GPHASE(0)
 #pragma unroll
     for (int g0 = 0; g0 < kGtTiles; g0 += kGtMG) {
       // every old value of a group of tiles before any write (a diagonal tile reads the mirrors of
@@ -1891,6 +1917,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
     }
     }
   }
+  TCI_GPHASE(1)
   __syncthreads();  // mb / mo reads, tile writes
   for (int j = t; j < P; j += NTH) mu[j] = na == 0.0 ? mb[j] : mo[j] + (mb[j] - mo[j]) * ((double)p.adaptint / nn);
   if (t == 0) {
@@ -1935,6 +1962,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
       if (bad && lane == 0) fail = 1;
     }
     __syncthreads();
+    TCI_GPHASE(2)
     if (fail) {
       ok = false;
       break;
@@ -1958,6 +1986,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
       }
     }
     __syncthreads();
+    TCI_GPHASE(3)
     {  // (3) trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj (4 MFMAs), round-robin over
        // waves, kGtBatch tiles at a time: every load of the batch is issued before the first store
        // (one memory round trip per batch, not per tile: the stores may alias later loads)
@@ -1993,6 +2022,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
       }
     }
     __syncthreads();
+    TCI_GPHASE(4)
   }
   if (ok) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
@@ -2020,6 +2050,10 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
     }
   }
   __syncthreads();
+  TCI_GPHASE(5)
+#undef TCI_GPHASE
+  if (TCI_ADAPT_PROFILE && t == 0 && st.prof != nullptr)
+    for (int q = 0; q < 6; ++q) atomicAdd((unsigned long long*)&st.prof[q], (unsigned long long)aph[q]);
   if (t == 0) st.nrej_win[c] = 0;
 }
 

@@ -10,6 +10,10 @@ namespace tci {
 
 // One workgroup (256 threads) per chain. All arrays are indexed by chain c; vectors have stride ld (= max parameter count P_max),
 // matrices stride ld*ld (row-major, P_c x P_c used).
+// Floats per chain of DramState::Rf: the packed triangle ld(ld+1)/2 rounded up to 256 floats, so a
+// chain's triangle starts 1 KiB-aligned and is copied to LDS in whole 1 KiB pieces (k_draws).
+constexpr int64_t dram_tri_stride(int64_t ld) { return (ld * (ld + 1) / 2 + 255) / 256 * 256; }
+
 struct DramState {
   int64_t n_chains;
   int64_t ld;
@@ -26,7 +30,7 @@ struct DramState {
   double* prior;           // prior SS of the current state
   double* sigma2;          // error variance (model.sigma2, :259)
   double* R;               // proposal Cholesky factor (upper, float-representable): proposal = theta + z * R
-  float* Rf;               // the same R as packed fp32 upper triangles (chain c at c * ld(ld+1)/2)
+  float* Rf;               // the same R as packed fp32 upper triangles (chain c at c * dram_tri_stride(ld))
   double* cov;             // running chain covariance / mean / weight (mcmcstat covupd)
   double* cmean;
   double* wsum;
