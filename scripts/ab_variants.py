@@ -62,6 +62,10 @@ VARIANTS = {
     "grp2": ["TCI_DRAW_PASSES_GR=2"],
     "grp7": ["TCI_DRAW_PASSES_GR=7"],
     "glds0": ["TCI_DRAWS_GLDS=0"],
+    "pf0": ["TCI_DRAWS_PF=0"],
+    "pf1": ["TCI_DRAWS_PF=1"],
+    "pf2": ["TCI_DRAWS_PF=2"],
+    "pf5": ["TCI_DRAWS_PF=5"],
 }
 
 

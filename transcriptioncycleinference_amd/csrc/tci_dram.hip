@@ -275,7 +275,9 @@ __device__ void load_R_f32(float* Rl, const DramState& st, int64_t c, int P) {
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 // top: the highest column tile of this call (tiles top, top-1, .. top+1-NWV*CT are computed):
 // (P + 15)/16 - 1 for one call; wider rows loop over tops (propose_block).
-template <int MT, int CT, int NWV, class Store>  // NWV: waves sharing the column tiles
+// PF > 0 (R in global memory): every k-step also loads the R values of all CT tiles PF k-steps
+// ahead, so an L2/HBM round trip overlaps PF k-steps' MFMAs instead of preceding them.
+template <int MT, int CT, int NWV, class Store, int PF = 0>  // NWV: waves sharing the column tiles; PF: prefetch depth
 __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const float* Rl, int P, int top, Store store) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int row = lane & 15, kq = lane >> 4;
@@ -294,11 +296,34 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[g][m] = f64x4{0.0, 0.0, 0.0, 0.0};
   int i0 = 0;
+  // raw R values of k-step i0n for every tile (inactive tiles read a valid clamped entry)
+  auto load_b = [&](int i0n, float* b) {
+    const int icn = min(i0n + kq, P - 1);
+    const int tof = tri_off(icn, P) - icn;
+#pragma unroll
+    for (int g = 0; g < CT; ++g) {
+      const int jc = min(max(16 * nt[g] + row, 0), P - 1);
+      b[g] = Rl[tof + (jc >= icn ? jc : icn)];
+    }
+  };
+  float bq[PF > 0 ? PF : 1][CT];  // bq[d]: k-step i0 + 4 d (rotated every step)
+#pragma unroll
+  for (int d = 0; d < PF; ++d) load_b(4 * d, bq[d]);
 #pragma unroll
   for (int ng = CT; ng >= 1; --ng) {
     for (; i0 <= kmx[ng - 1]; i0 += 4) {  // tiles g < ng still need k-step i0
       const int i = i0 + kq;
       const int ic = i < P ? i : P - 1;
+      float bcur[CT];
+      if (PF > 0) {
+#pragma unroll
+        for (int g = 0; g < CT; ++g) bcur[g] = bq[0][g];
+#pragma unroll
+        for (int d = 0; d + 1 < PF; ++d)
+#pragma unroll
+          for (int g = 0; g < CT; ++g) bq[d][g] = bq[d + 1][g];
+        load_b(i0 + 4 * PF, bq[PF > 0 ? PF - 1 : 0]);
+      }
       double a[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
@@ -311,7 +336,7 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
       for (int g = 0; g < ng; ++g) {
         const int j = 16 * nt[g] + row;
         const int jc = j < P ? j : P - 1;
-        const float rv = Rl[toff + (jc >= ic ? jc : ic)];
+        const float rv = PF > 0 ? bcur[g] : Rl[toff + (jc >= ic ? jc : ic)];
         const double b = (i <= j && j < P) ? (double)rv : 0.0;
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[g][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b, acc[g][m], 0, 0, 0);
@@ -659,6 +684,9 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
 #ifndef TCI_DRAWS_GLDS
 #define TCI_DRAWS_GLDS 1  // stage R by LDS-DMA (load_R_glds); 0 = through registers (A/B)
 #endif
+#ifndef TCI_DRAWS_PF
+#define TCI_DRAWS_PF 2  // R from global memory: R values prefetched this many k-steps ahead (mfma_zr PF); 0 = off
+#endif
 #ifndef TCI_DRAWS_FLAT
 #define TCI_DRAWS_FLAT 0  // A/B only: 1 = one z*R call through a selected (generic) R pointer
 #endif
@@ -740,7 +768,7 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
         mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, rl ? (const float*)Rl : Rg, P, top, put);
 #else
         if (rl) mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rl, P, top, put);
-        else mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rg, P, top, put);
+        else mfma_zr<kDrawMT, kDrawCT, kDrawWaves, decltype(put), TCI_DRAWS_PF>(Z, L, 2 * ns, Rg, P, top, put);
 #endif
       }
     for (int k = w; k < ns; k += kDrawWaves) {
