@@ -63,6 +63,11 @@ VARIANTS = {
     "grp7": ["TCI_DRAW_PASSES_GR=7"],
     "glds0": ["TCI_DRAWS_GLDS=0"],
     "pf0": ["TCI_DRAWS_PF=0"],
+    "wp4": ["TCI_DRAW_PASSES_WALK=4"],
+    "wp7": ["TCI_DRAW_PASSES_WALK=7"],
+    "gtw16t5": ["TCI_GT_WAVES=16", "TCI_GT_TILES=5"],
+    "gtw16t8": ["TCI_GT_WAVES=16", "TCI_GT_TILES=8"],
+    "gtw16t10": ["TCI_GT_WAVES=16", "TCI_GT_TILES=10"],
     "pf1": ["TCI_DRAWS_PF=1"],
     "pf2": ["TCI_DRAWS_PF=2"],
     "pf5": ["TCI_DRAWS_PF=5"],

@@ -717,7 +717,15 @@ __host__ __device__ inline bool draws_r_lds(int64_t L) {
 __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
   return (2 * kDrawSteps * L) * 8 + (draws_r_lds(L) ? dram_tri_stride(L) * 4 : 0) + 16;
 }
-__host__ __device__ inline int draws_passes(int64_t ld) { return draws_r_lds(ld) ? kDrawPasses : kDrawPassesGR; }
+#ifndef TCI_DRAW_PASSES_WALK
+#define TCI_DRAW_PASSES_WALK 4
+#endif
+// WALK (thousands of chains, one draws workgroup per CU): passes per workgroup with R in LDS,
+// so R is staged once per 64 steps (configs 4/5: 174.3 -> 171.6 us per step; 7 passes: 171.9)
+constexpr int kDrawPassesWalk = TCI_DRAW_PASSES_WALK;
+__host__ __device__ inline int draws_passes(int64_t ld, bool walk) {
+  return !draws_r_lds(ld) ? kDrawPassesGR : walk ? kDrawPassesWalk : kDrawPasses;
+}
 
 // NWD waves per workgroup: 4 for the FUSED engine (299 TestData chains: 100.6 vs 105.4 ms per 20k
 // steps with 8), 8 for WALK (10,000 chains, one workgroup per CU at P = 207: 175 vs 188 ms per
@@ -1408,7 +1416,7 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
   if (lds > 48 * 1024 &&
       hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return TCI_EHIP;
-  const int npass = draws_passes(st.ld);
+  const int npass = draws_passes(st.ld, p.walk != 0);
   const int64_t per_wg = (int64_t)kDrawSteps * npass;  // <= the workgroup's threads (scalar draws)
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
   hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(p.walk ? 512 : 256), lds, stream, st, p, s_begin, s_end,
@@ -1790,7 +1798,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8
 #ifndef TCI_GT_TILES
 #define TCI_GT_TILES 8
 #endif
-constexpr int kGtWaves = 8, kGtTiles = TCI_GT_TILES;
+#ifndef TCI_GT_WAVES
+#define TCI_GT_WAVES 8
+#endif
+constexpr int kGtWaves = TCI_GT_WAVES, kGtTiles = TCI_GT_TILES;
 #ifndef TCI_GT_BATCH
 #define TCI_GT_BATCH 2
 #endif
