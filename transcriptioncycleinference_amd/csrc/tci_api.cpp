@@ -584,7 +584,6 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(ss, double, n);
   TCI_ALLOC(prior, double, n);
   TCI_ALLOC(sigma2, double, n);
-  TCI_ALLOC(R, double, n * L2);
   TCI_ALLOC(Rf, float, n * tci::dram_tri_stride(L));
   TCI_ALLOC(cov, double, n * L2);
   TCI_ALLOC(work, double, p_max_all > 208 ? n * (size_t)((L + 15) / 16 * 16) * ((L + 15) / 16 * 16) : 1);
@@ -778,7 +777,19 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   if (out->final_theta) TCI_HIP(ctx, hipMemcpy(out->final_theta, st.theta, n * L * sizeof(double), hipMemcpyDeviceToHost));
   if (st.chain_out && out->chain)
     TCI_HIP(ctx, hipMemcpy(out->chain, st.chain_out, (size_t)n_keep * n * L * sizeof(double), hipMemcpyDeviceToHost));
-  if (out->qcov_R) TCI_HIP(ctx, hipMemcpy(out->qcov_R, st.R, n * L2 * sizeof(double), hipMemcpyDeviceToHost));
+  if (out->qcov_R) {  // the device keeps R as packed fp32 upper triangles (exact: R is float-representable)
+    const int64_t ts = tci::dram_tri_stride((int64_t)L);
+    std::vector<float> rf((size_t)n * ts);
+    TCI_HIP(ctx, hipMemcpy(rf.data(), st.Rf, rf.size() * sizeof(float), hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < n; ++c) {
+      double* R = out->qcov_R + c * L2;
+      std::fill(R, R + L2, 0.0);
+      const int64_t P = npar[c];
+      const float* src = rf.data() + c * ts;
+      for (int64_t i = 0, e = 0; i < P; ++i)
+        for (int64_t j = i; j < P; ++j, ++e) R[i * L + j] = (double)src[e];
+    }
+  }
   if (st.s2_out && out->s2chain)
     TCI_HIP(ctx, hipMemcpy(out->s2chain, st.s2_out, (size_t)n_keep * n * sizeof(double), hipMemcpyDeviceToHost));
   return TCI_OK;

@@ -237,8 +237,12 @@ __device__ __forceinline__ double f32_round(double x) { return (double)(float)x;
 __device__ __forceinline__ int tri_off(int i, int P) { return i * P - (i * (i - 1)) / 2; }
 __host__ __device__ inline int64_t tri_stride(int64_t ld) { return dram_tri_stride(ld); }
 __device__ __forceinline__ void store_R(const DramState& st, int64_t c, int P, int i, int j, double v) {
-  st.R[c * st.ld * st.ld + (int64_t)i * st.ld + j] = v;
   if (j >= i) st.Rf[c * tri_stride(st.ld) + tri_off(i, P) + j - i] = (float)v;
+}
+// Burn-in scaling R <- f32_round(R * s), on the packed triangle (the lower triangle is zero).
+__device__ __forceinline__ void scale_R(const DramState& st, int64_t c, int P, double s, int t, int nth) {
+  float* Rf = st.Rf + c * tri_stride(st.ld);
+  for (int e = t; e < P * (P + 1) / 2; e += nth) Rf[e] = (float)((double)Rf[e] * s);
 }
 // The same copy by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction, no registers):
 // every piece is in flight at once, and the caller's next work (the draws pass's normals) runs
@@ -441,12 +445,8 @@ __global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* _
   if (c >= st.n_chains) return;
   const int64_t ld = st.ld;
   const int P = st.npar[c];
-  double* R = st.R + c * ld * ld;
   double* cv = st.cov + c * ld * ld;
-  for (int64_t e = threadIdx.x; e < ld * ld; e += kThreads) {
-    R[e] = 0.0;
-    cv[e] = 0.0;
-  }
+  for (int64_t e = threadIdx.x; e < ld * ld; e += kThreads) cv[e] = 0.0;
   for (int64_t e = threadIdx.x; e < tri_stride(ld); e += kThreads) st.Rf[c * tri_stride(ld) + e] = 0.0f;
   __syncthreads();
   for (int j = threadIdx.x; j < P; j += kThreads) {
@@ -1674,13 +1674,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8
     double s = 1.0;
     if (rate > 0.95) s = 1.0 / p.burnin_scale;
     else if (rate < 0.05) s = p.burnin_scale;
-    if (s != 1.0) {
-      double* R = st.R + c * ld * ld;
-      for (int64_t e = t; e < (int64_t)P * P; e += NTH) {
-        const int i = (int)(e / P), j = (int)(e % P);
-        store_R(st, c, P, i, j, f32_round(R[(int64_t)i * ld + j] * s));
-      }
-    }
+    if (s != 1.0) scale_R(st, c, P, s, t, NTH);
     __syncthreads();
     if (t == 0) st.nrej_win[c] = 0;
     return;
@@ -1969,13 +1963,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
     double s = 1.0;
     if (rate > 0.95) s = 1.0 / p.burnin_scale;
     else if (rate < 0.05) s = p.burnin_scale;
-    if (s != 1.0) {
-      double* R = st.R + c * ld * ld;
-      for (int64_t e = t; e < (int64_t)P * P; e += NTH) {
-        const int i = (int)(e / P), j = (int)(e % P);
-        store_R(st, c, P, i, j, f32_round(R[(int64_t)i * ld + j] * s));
-      }
-    }
+    if (s != 1.0) scale_R(st, c, P, s, t, NTH);
     __syncthreads();
     if (t == 0) st.nrej_win[c] = 0;
     return;

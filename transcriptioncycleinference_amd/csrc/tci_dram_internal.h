@@ -29,8 +29,9 @@ struct DramState {
   double* ss;              // SS of the current state
   double* prior;           // prior SS of the current state
   double* sigma2;          // error variance (model.sigma2, :259)
-  double* R;               // proposal Cholesky factor (upper, float-representable): proposal = theta + z * R
-  float* Rf;               // the same R as packed fp32 upper triangles (chain c at c * dram_tri_stride(ld))
+  float* Rf;               // proposal Cholesky factor R (upper, float-representable: proposal = theta + z * R)
+                           // as packed fp32 upper triangles (chain c at c * dram_tri_stride(ld)); the
+                           // [ld][ld] double form is built on the host for the results only
   double* cov;             // running chain covariance / mean / weight (mcmcstat covupd)
   double* cmean;
   double* wsum;
