@@ -21,9 +21,10 @@
 //             covupd over all chain rows so far, R = chol(cov + qcovadj*I) * adascale
 //   prior     sum(((theta - mu)./sig).^2) over parameters with finite sig (dR: N(0, 50), :254)
 // The proposal factor R is kept with float-representable entries (rounded once when it is set),
-// so a chain's R fits in LDS as fp32 (P(P+1)/2 floats) for the proposal products; the proposal
-// covariance is then R'R of that rounded R, consistently in both stages (a 1e-7-relative change
-// of the proposal shape; the sampler stays exact for it).
+// so a chain's R is held exactly as a packed fp32 upper triangle (P(P+1)/2 floats: DramState::Rf,
+// the only device copy) and fits in LDS for the proposal products; the proposal covariance is then
+// R'R of that rounded R, consistently in both stages (a 1e-7-relative change of the proposal
+// shape; the sampler stays exact for it).
 // Randomness: Philox4x32-10 keyed by (seed), counter (chain, step, purpose, index) -- the
 // stream is reproducible and independent of launch geometry (MATLAB's MT19937 is not
 // reproducible here, so chain parity with the reference is statistical only).
