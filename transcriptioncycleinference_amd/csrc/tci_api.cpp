@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -38,6 +39,11 @@ struct tci_ctx {
   double* d_out0 = nullptr;
   double* d_out1 = nullptr;
   size_t cap_theta = 0, cap_cell = 0, cap_active = 0, cap_out0 = 0, cap_out1 = 0;
+  // small batches of the host-pointer entry points: one pinned, device-mapped buffer the kernel
+  // reads and writes in place (no copy launches; tci_ss_batch)
+  char* h_io = nullptr;
+  char* d_io = nullptr;
+  size_t cap_io = 0;
   std::string err;
 };
 
@@ -113,6 +119,28 @@ int ensure(tci_ctx* ctx, T** p, size_t* cap, size_t need) {
   size_t n = std::max(need, (size_t)1024);
   TCI_HIP(ctx, hipMalloc((void**)p, n * sizeof(T)));
   *cap = n;
+  return TCI_OK;
+}
+
+// Bytes of theta + ids + flags + SS per call up to which tci_ss_batch works in place in pinned host
+// memory (TCI_ZERO_COPY_MAX overrides; 0 disables).
+size_t zero_copy_max() {
+  static const size_t v = [] {
+    const char* e = std::getenv("TCI_ZERO_COPY_MAX");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)1024 * 1024;
+  }();
+  return v;
+}
+
+int ensure_io(tci_ctx* ctx, size_t need) {
+  if (need <= ctx->cap_io) return TCI_OK;
+  if (ctx->h_io) (void)hipHostFree(ctx->h_io);
+  ctx->h_io = ctx->d_io = nullptr;
+  ctx->cap_io = 0;
+  const size_t n = std::max(need, (size_t)64 * 1024);
+  TCI_HIP(ctx, hipHostMalloc((void**)&ctx->h_io, n, hipHostMallocMapped | hipHostMallocCoherent));
+  TCI_HIP(ctx, hipHostGetDevicePointer((void**)&ctx->d_io, ctx->h_io, 0));
+  ctx->cap_io = n;
   return TCI_OK;
 }
 
@@ -349,6 +377,7 @@ int tci_destroy(tci_ctx* ctx) {
   for (void* q : {(void*)ctx->dbuf, (void*)ctx->d_theta, (void*)ctx->d_cell, (void*)ctx->d_active,
                   (void*)ctx->d_out0, (void*)ctx->d_out1})
     if (q) (void)hipFree(q);
+  if (ctx->h_io) (void)hipHostFree(ctx->h_io);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return TCI_OK;
@@ -388,6 +417,23 @@ int tci_ss_batch(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int3
   if (rc != TCI_OK) return rc;
   TCI_HIP(ctx, hipSetDevice(ctx->device));
   const size_t nth = (size_t)B * (size_t)ld_theta;
+  // layout of the zero-copy buffer: theta | SS | cell ids | active flags (8-byte aligned blocks)
+  const size_t o_ss = nth * 8, o_cell = o_ss + (size_t)B * 8, o_act = o_cell + ((size_t)B * 4 + 7) / 8 * 8;
+  if (o_act + (size_t)B <= zero_copy_max()) {
+    // a small batch (the drop-in tci_ssfun is B = 1): the kernel reads theta/ids/flags from pinned
+    // host memory and writes the SS there; one launch and one synchronisation per call
+    if ((rc = ensure_io(ctx, o_act + (size_t)B)) != TCI_OK) return rc;
+    std::memcpy(ctx->h_io, theta, nth * 8);
+    std::memcpy(ctx->h_io + o_cell, cell_id, (size_t)B * 4);
+    if (active) std::memcpy(ctx->h_io + o_act, active, (size_t)B);
+    rc = run(ctx, tci::MODE_SS, (const double*)ctx->d_io, ld_theta, (const int32_t*)(ctx->d_io + o_cell),
+             active ? (const uint8_t*)(ctx->d_io + o_act) : nullptr, B, (double*)(ctx->d_io + o_ss), nullptr, 0,
+             (void*)ctx->stream);
+    if (rc != TCI_OK) return rc;
+    TCI_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::memcpy(ss_out, ctx->h_io + o_ss, (size_t)B * 8);
+    return TCI_OK;
+  }
   if ((rc = ensure(ctx, &ctx->d_theta, &ctx->cap_theta, nth)) != TCI_OK) return rc;
   if ((rc = ensure(ctx, &ctx->d_cell, &ctx->cap_cell, (size_t)B)) != TCI_OK) return rc;
   if ((rc = ensure(ctx, &ctx->d_active, &ctx->cap_active, (size_t)B)) != TCI_OK) return rc;
