@@ -63,6 +63,8 @@ VARIANTS = {
     "grp7": ["TCI_DRAW_PASSES_GR=7"],
     "glds0": ["TCI_DRAWS_GLDS=0"],
     "pf0": ["TCI_DRAWS_PF=0"],
+    "gtp1": ["TCI_GT_PANELS=1"],
+    "gtp3": ["TCI_GT_PANELS=3"],
     "wp4": ["TCI_DRAW_PASSES_WALK=4"],
     "wp7": ["TCI_DRAW_PASSES_WALK=7"],
     "gtw16t5": ["TCI_GT_WAVES=16", "TCI_GT_TILES=5"],

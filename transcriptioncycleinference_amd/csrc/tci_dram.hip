@@ -36,6 +36,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "tci_dram_internal.h"
 #include "tci_eval.h"
@@ -1808,6 +1809,10 @@ constexpr int kGtPer = TCI_GT_PER;  // window loads in flight per thread
 #ifndef TCI_GT_MG
 #define TCI_GT_MG 1
 #endif
+#ifndef TCI_GT_PANELS
+#define TCI_GT_PANELS 3
+#endif
+constexpr int kGtPanels = TCI_GT_PANELS;  // Cholesky panels per trailing pass (1 or 2)
 constexpr int kGtMG = TCI_GT_MG;  // merge group: tiles whose old covariance values are read together
 __host__ __device__ inline int64_t gt_lt(int64_t ld) { return (ld + 15) / 16 * 16; }  // tile-grid side
 __host__ __device__ inline int gt_rows(int64_t P) {  // window rows per LDS batch
@@ -1970,10 +1975,14 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
     return;
   }
   __syncthreads();
-  // ---- blocked Cholesky U'U of the tile grid
-  bool ok = true;
-  for (int pk = 0; pk < NT; ++pk) {
-    if (w == 0) {  // (1) the diagonal tile, factored in wave 0's registers
+  // ---- blocked Cholesky U'U of the tile grid, two panels per trailing pass (kGtPanels): panel pk
+  //      is factored, row pk + 1 takes its update, panel pk + 1 is factored, and every tile below
+  //      takes both rank-16 updates in one read-modify-write (8 MFMAs in panel order: the same bits
+  //      as two passes, half the tile traffic of the trailing updates)
+  // (1) + (2): the diagonal tile of panel pk in wave 0's registers, then the panel's row tiles
+  //     (pk, tj > pk): U_pk' X = A -> X, one column per lane; false if a pivot failed
+  auto factor_panel = [&](int pk) -> bool {
+    if (w == 0) {
       double* A = tile(pk, pk);
       double dt[4];
 #pragma unroll
@@ -1991,66 +2000,92 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
     }
     __syncthreads();
     TCI_GPHASE(2)
-    if (fail) {
-      ok = false;
-      break;
-    }
-    {  // (2) the panel's row tiles (pk, tj > pk): U_pk' X = A -> X, one column per lane
-      const int g = w * 4 + kq;  // 16-lane group 0 .. 4 NW - 1
-      for (int tj = pk + 1 + g; tj < NT; tj += 4 * NW) {
-        asm volatile("" ::: "memory");  // Dt is re-read per tile, not hoisted into 120 registers
-        double* A = tile(pk, tj);
-        double x[16];
+    if (fail) return false;
+    const int g = w * 4 + kq;  // 16-lane group 0 .. 4 NW - 1
+    for (int tj = pk + 1 + g; tj < NT; tj += 4 * NW) {
+      asm volatile("" ::: "memory");  // Dt is re-read per tile, not hoisted into 120 registers
+      double* A = tile(pk, tj);
+      double x[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = A[k * 16 + row];
+      for (int k = 0; k < 16; ++k) x[k] = A[k * 16 + row];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          x[k] = x[k] * rdg[k];
+      for (int k = 0; k < 16; ++k) {
+        x[k] = x[k] * rdg[k];
 #pragma unroll
-          for (int m = k + 1; m < 16; ++m) x[m] = fma(-Dt[k * 16 + m], x[k], x[m]);
-        }
-#pragma unroll
-        for (int k = 0; k < 16; ++k) A[k * 16 + row] = x[k];
+        for (int m = k + 1; m < 16; ++m) x[m] = fma(-Dt[k * 16 + m], x[k], x[m]);
       }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) A[k * 16 + row] = x[k];
     }
     __syncthreads();
     TCI_GPHASE(3)
-    {  // (3) trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj (4 MFMAs), round-robin over
-       // waves, kGtBatch tiles at a time: every load of the batch is issued before the first store
-       // (one memory round trip per batch, not per tile: the stores may alias later loads)
-      const int m = NT - pk - 1, Ttr = m * (m + 1) / 2;
-      for (int k0 = w; k0 < Ttr; k0 += NW * kGtBatch) {
-        double* Ap[kGtBatch];
-        f64x4 acc[kGtBatch];
-        double xi[kGtBatch][4], xj[kGtBatch][4];
+    return true;
+  };
+  // (3) trailing tiles (ti, tj), r0 <= ti <= tj (ti < r1), A -= X_ti' X_tj by panels pa .. pa + NP - 1,
+  //     round-robin over waves, kGtBatch tiles at a time: every load of the batch is issued before
+  //     the first store (one memory round trip per batch, not per tile: the stores may alias later
+  //     loads)
+  auto trail = [&](auto np_c, int pa, int r0, int r1) {
+    constexpr int NP = decltype(np_c)::value;
+    constexpr int BT = NP <= 2 ? kGtBatch : 1;  // tiles per batch (register budget)
+    const int m = NT - r0, Ttr = (r1 - r0) * (2 * m - (r1 - r0) + 1) / 2;  // rows r0 .. r1 - 1 of the triangle
+    for (int k0 = w; k0 < Ttr; k0 += NW * BT) {
+      double* Ap[BT];
+      f64x4 acc[BT];
+      double xi[BT][NP][4], xj[BT][NP][4];
 #pragma unroll
-        for (int g = 0; g < kGtBatch; ++g) {
-          const int k = k0 + g * NW;
-          if (k >= Ttr) break;  // uniform
-          int ti, tj;
-          tri_tile(k, m, pk + 1, ti, tj);
-          Ap[g] = tile(ti, tj);
-          const double* Xi = tile(pk, ti);
-          const double* Xj = tile(pk, tj);
+      for (int g = 0; g < BT; ++g) {
+        const int k = k0 + g * NW;
+        if (k >= Ttr) break;  // uniform
+        int ti, tj;
+        tri_tile(k, m, r0, ti, tj);
+        Ap[g] = tile(ti, tj);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[g][q] = Ap[g][(kq + 4 * q) * 16 + row];
+#pragma unroll
+        for (int h = 0; h < NP; ++h) {
+          const double* Xi = tile(pa + h, ti);
+          const double* Xj = tile(pa + h, tj);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            acc[g][q] = Ap[g][(kq + 4 * q) * 16 + row];
-            xi[g][q] = Xi[(4 * q + kq) * 16 + row];
-            xj[g][q] = Xj[(4 * q + kq) * 16 + row];
+            xi[g][h][q] = Xi[(4 * q + kq) * 16 + row];
+            xj[g][h][q] = Xj[(4 * q + kq) * 16 + row];
           }
         }
+      }
 #pragma unroll
-        for (int g = 0; g < kGtBatch; ++g) {
-          if (k0 + g * NW >= Ttr) break;
+      for (int g = 0; g < BT; ++g) {
+        if (k0 + g * NW >= Ttr) break;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(-xi[g][q], xj[g][q], acc[g], 0, 0, 0);
+        for (int h = 0; h < NP; ++h)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) Ap[g][(kq + 4 * q) * 16 + row] = acc[g][q];
-        }
+          for (int q = 0; q < 4; ++q)
+            acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(-xi[g][h][q], xj[g][h][q], acc[g], 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Ap[g][(kq + 4 * q) * 16 + row] = acc[g][q];
       }
     }
     __syncthreads();
     TCI_GPHASE(4)
+  };
+  auto trail_n = [&](int np, int pa, int r0, int r1) {  // np panels pa .. pa + np - 1
+    if (np <= 0 || r0 >= r1) return;
+    switch (np) {
+      case 1: trail(std::integral_constant<int, 1>{}, pa, r0, r1); break;
+      case 2: trail(std::integral_constant<int, 2>{}, pa, r0, r1); break;
+      case 3: trail(std::integral_constant<int, 3>{}, pa, r0, r1); break;
+      default: trail(std::integral_constant<int, 4>{}, pa, r0, r1); break;
+    }
+  };
+  static_assert(kGtPanels >= 1 && kGtPanels <= 4, "panels per trailing pass (4 spills at the 128-VGPR budget)");
+  bool ok = true;
+  for (int pk = 0; pk < NT && ok; pk += kGtPanels) {
+    const int np = min(kGtPanels, NT - pk);
+    for (int j = 0; j < np && ok; ++j) {
+      trail_n(j, pk, pk + j, pk + j + 1);  // row pk + j by panels pk .. pk + j - 1
+      ok = factor_panel(pk + j);
+    }
+    if (ok) trail_n(np, pk, pk + np, NT);  // the rows below by all np panels
   }
   if (ok) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
