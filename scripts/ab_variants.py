@@ -65,6 +65,9 @@ VARIANTS = {
     "pf0": ["TCI_DRAWS_PF=0"],
     "gtp1": ["TCI_GT_PANELS=1"],
     "gtp3": ["TCI_GT_PANELS=3"],
+    "gtp4": ["TCI_GT_PANELS=4"],
+    "gtp4w3": ["TCI_GT_PANELS=4", "TCI_GT_WPE=3"],
+    "gtp3w3": ["TCI_GT_PANELS=3", "TCI_GT_WPE=3"],
     "wp4": ["TCI_DRAW_PASSES_WALK=4"],
     "wp7": ["TCI_DRAW_PASSES_WALK=7"],
     "gtw16t5": ["TCI_GT_WAVES=16", "TCI_GT_TILES=5"],

@@ -1812,7 +1812,10 @@ constexpr int kGtPer = TCI_GT_PER;  // window loads in flight per thread
 #ifndef TCI_GT_PANELS
 #define TCI_GT_PANELS 3
 #endif
-constexpr int kGtPanels = TCI_GT_PANELS;  // Cholesky panels per trailing pass (1 or 2)
+#ifndef TCI_GT_WPE
+#define TCI_GT_WPE 4
+#endif
+constexpr int kGtPanels = TCI_GT_PANELS;  // Cholesky panels per trailing pass (1 .. 4)
 constexpr int kGtMG = TCI_GT_MG;  // merge group: tiles whose old covariance values are read together
 __host__ __device__ inline int64_t gt_lt(int64_t ld) { return (ld + 15) / 16 * 16; }  // tile-grid side
 __host__ __device__ inline int gt_rows(int64_t P) {  // window rows per LDS batch
@@ -1835,7 +1838,7 @@ __device__ __forceinline__ void tri_tile(int k, int n, int r0, int& ti, int& tj)
   tj = r0 + i + k;
 }
 
-__global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4))) void k_adapt_gt(DramState st,
+__global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(TCI_GT_WPE))) void k_adapt_gt(DramState st,
                                                                                                     DramParams p) {
   constexpr int NW = kGtWaves, NTH = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) double dyn[];
@@ -1975,10 +1978,10 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
     return;
   }
   __syncthreads();
-  // ---- blocked Cholesky U'U of the tile grid, two panels per trailing pass (kGtPanels): panel pk
-  //      is factored, row pk + 1 takes its update, panel pk + 1 is factored, and every tile below
-  //      takes both rank-16 updates in one read-modify-write (8 MFMAs in panel order: the same bits
-  //      as two passes, half the tile traffic of the trailing updates)
+  // ---- blocked Cholesky U'U of the tile grid, kGtPanels (3) panels per trailing pass: panel pk is
+  //      factored, row pk + 1 takes its update, panel pk + 1 is factored, ..., and every tile below
+  //      takes all the group's rank-16 updates in one read-modify-write (4 MFMAs per panel, in panel
+  //      order: the same bits as one pass per panel, 1/kGtPanels of the trailing tile traffic)
   // (1) + (2): the diagonal tile of panel pk in wave 0's registers, then the panel's row tiles
   //     (pk, tj > pk): U_pk' X = A -> X, one column per lane; false if a pivot failed
   auto factor_panel = [&](int pk) -> bool {
