@@ -70,6 +70,7 @@ VARIANTS = {
     "gtp3w3": ["TCI_GT_PANELS=3", "TCI_GT_WPE=3"],
     "gtt10p4": ["TCI_GT_TILES=10", "TCI_GT_PER=4"],
     "gtt10": ["TCI_GT_TILES=10"],
+    "gtdirect": ["TCI_GT_DIRECT=1"],
     "wp4": ["TCI_DRAW_PASSES_WALK=4"],
     "wp7": ["TCI_DRAW_PASSES_WALK=7"],
     "gtw16t5": ["TCI_GT_WAVES=16", "TCI_GT_TILES=5"],

@@ -1815,7 +1815,13 @@ constexpr int kGtPer = TCI_GT_PER;  // window loads in flight per thread
 #ifndef TCI_GT_WPE
 #define TCI_GT_WPE 4
 #endif
+#ifndef TCI_GT_DIRECT
+#define TCI_GT_DIRECT 0
+#endif
 constexpr int kGtPanels = TCI_GT_PANELS;  // Cholesky panels per trailing pass (1 .. 4)
+// 1: the scatter writes only cov; each tile's first touch in the Cholesky (panel group 0) reads
+// cov + qcovadj I from it, so the tile grid is not written and re-read once (same bits)
+constexpr bool kGtDirect = TCI_GT_DIRECT != 0;
 constexpr int kGtMG = TCI_GT_MG;  // merge group: tiles whose old covariance values are read together
 __host__ __device__ inline int64_t gt_lt(int64_t ld) { return (ld + 15) / 16 * 16; }  // tile-grid side
 __host__ __device__ inline int gt_rows(int64_t P) {  // window rows per LDS batch
@@ -1954,7 +1960,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
         } else {
           a = i == j ? 1.0 : 0.0;
         }
-        A[(kq + 4 * q) * 16 + row] = a;
+        if (!kGtDirect) A[(kq + 4 * q) * 16 + row] = a;
       }
     }
     }
@@ -1984,12 +1990,23 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
   //      order: the same bits as one pass per panel, 1/kGtPanels of the trailing tile traffic)
   // (1) + (2): the diagonal tile of panel pk in wave 0's registers, then the panel's row tiles
   //     (pk, tj > pk): U_pk' X = A -> X, one column per lane; false if a pivot failed
+  // element (16 ti + lr, 16 tj + row) of cov + qcovadj I (identity past P): a tile's value before
+  // its first Cholesky touch, read from cov (upper triangle; a diagonal tile's lower half from the
+  // mirror), the value the scatter's merge wrote there
+  auto src = [&](int ti, int tj, int lr) -> double {
+    const int i = 16 * ti + lr, j = 16 * tj + row;
+    if (i < P && j < P) {
+      const double cv = cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i];
+      return cv + (i == j ? p.qcovadj : 0.0);
+    }
+    return i == j ? 1.0 : 0.0;
+  };
   auto factor_panel = [&](int pk) -> bool {
     if (w == 0) {
       double* A = tile(pk, pk);
       double dt[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dt[q] = A[(kq + 4 * q) * 16 + row];
+      for (int q = 0; q < 4; ++q) dt[q] = kGtDirect && pk == 0 ? src(pk, pk, kq + 4 * q) : A[(kq + 4 * q) * 16 + row];
       bool bad = false;
       chol16_step<0>(dt, lane, rdg, bad);
       wave_sync();
@@ -2010,7 +2027,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
       double* A = tile(pk, tj);
       double x[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) x[k] = A[k * 16 + row];
+      for (int k = 0; k < 16; ++k) x[k] = kGtDirect && pk == 0 ? src(pk, tj, k) : A[k * 16 + row];
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         x[k] = x[k] * rdg[k];
@@ -2028,8 +2045,9 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
   //     round-robin over waves, kGtBatch tiles at a time: every load of the batch is issued before
   //     the first store (one memory round trip per batch, not per tile: the stores may alias later
   //     loads)
-  auto trail = [&](auto np_c, int pa, int r0, int r1) {
+  auto trail = [&](auto np_c, auto first_c, int pa, int r0, int r1) {
     constexpr int NP = decltype(np_c)::value;
+    constexpr bool FIRST = decltype(first_c)::value;  // the tiles' first touch: read cov (kGtDirect)
     constexpr int BT = NP <= 2 ? kGtBatch : 1;  // tiles per batch (register budget)
     const int m = NT - r0, Ttr = (r1 - r0) * (2 * m - (r1 - r0) + 1) / 2;  // rows r0 .. r1 - 1 of the triangle
     for (int k0 = w; k0 < Ttr; k0 += NW * BT) {
@@ -2044,7 +2062,8 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
         tri_tile(k, m, r0, ti, tj);
         Ap[g] = tile(ti, tj);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[g][q] = Ap[g][(kq + 4 * q) * 16 + row];
+        for (int q = 0; q < 4; ++q)
+          acc[g][q] = FIRST ? src(ti, tj, kq + 4 * q) : Ap[g][(kq + 4 * q) * 16 + row];
 #pragma unroll
         for (int h = 0; h < NP; ++h) {
           const double* Xi = tile(pa + h, ti);
@@ -2073,11 +2092,15 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
   };
   auto trail_n = [&](int np, int pa, int r0, int r1) {  // np panels pa .. pa + np - 1
     if (np <= 0 || r0 >= r1) return;
+    const auto go = [&](auto np_c) {
+      if (kGtDirect && pa == 0) trail(np_c, std::true_type{}, pa, r0, r1);
+      else trail(np_c, std::false_type{}, pa, r0, r1);
+    };
     switch (np) {
-      case 1: trail(std::integral_constant<int, 1>{}, pa, r0, r1); break;
-      case 2: trail(std::integral_constant<int, 2>{}, pa, r0, r1); break;
-      case 3: trail(std::integral_constant<int, 3>{}, pa, r0, r1); break;
-      default: trail(std::integral_constant<int, 4>{}, pa, r0, r1); break;
+      case 1: go(std::integral_constant<int, 1>{}); break;
+      case 2: go(std::integral_constant<int, 2>{}); break;
+      case 3: go(std::integral_constant<int, 3>{}); break;
+      default: go(std::integral_constant<int, 4>{}); break;
     }
   };
   static_assert(kGtPanels >= 1 && kGtPanels <= 4, "panels per trailing pass (4 spills at the 128-VGPR budget)");
