@@ -229,8 +229,9 @@ def end_to_end(lk, n_steps: int, seed: int, reduce=None):
         dev_s, wall = reduce(dev_s, "max"), reduce(wall, "max")
         evals, chains = int(reduce(evals, "sum")), int(reduce(chains, "sum"))
     return {"n_steps": n_steps, "chains": chains, "device_s": dev_s, "wall_s": wall,
-            "ssfun_evals": evals, "value": evals / dev_s, "unit": "SS evals/s",
-            "us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
+            "ssfun_evals": evals, "value": evals / wall, "unit": "SS evals/s (wall time, SURVEY §8(d)(ii))",
+            "us_per_step": wall * 1e6 / max(n_steps - 1, 1),
+            "device_value": evals / dev_s, "device_us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
             "accept_rate_median_rank0": float(np.median(fr.accept_rate))}
 
 
@@ -324,14 +325,56 @@ def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_s
         t0 = time.perf_counter()
         fr = fit(lk, n_steps=n_steps, n_burn=max(1, n_steps // 20), seed=cfg, opts=DramOptions(engine=engine))
         wall = reduce(time.perf_counter() - t0, "max")
+        # output checks (untimed): every chain's summaries and final state finite and in bounds, and
+        # the GPU SS of a sample of final states, which the cpu_baseline leg re-evaluates on the oracle
+        fin = fr.final_theta
+        ok = bool(np.all([np.isfinite(r["mean_v"]) and np.isfinite(r["mean_sigma"]) and np.all(np.isfinite(r["mean_dR"]))
+                          for r in fr.MCMCresults]))
+        lens = cells.lengths[fr.cell_index]
+        ok = ok and all(np.all(np.isfinite(fin[k, :7 + n])) for k, n in enumerate(lens))
+        sample = np.linspace(0, len(fr.cell_index) - 1, min(256, len(fr.cell_index))).astype(np.int64)
+        s_theta = np.ascontiguousarray(fin[sample])
+        s_cid = fr.cell_index[sample].astype(np.int32)
+        s_ss = lk.ss_batch(s_theta, s_cid)
+        ok = ok and bool(np.all(np.isfinite(s_ss)))
     dev_s, evals = reduce(fr.elapsed_ms * 1e-3, "max"), int(reduce(fr.n_evals, "sum"))
-    return {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points, construct {construct.name}, "
-                        f"{hi - lo} chains on rank 0, {n_steps} steps"
-                        + ("" if n_steps >= 200000 else " (bounded sample of the configured 200k)"),
-            "n_steps": n_steps, "engine": engine, "chains": int(reduce(len(fr.MCMCresults), "sum")), "device_s": dev_s,
-            "wall_s": wall, "ssfun_evals": evals, "value": evals / dev_s, "unit": "SS evals/s", "scaling": "strong",
-            "us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
-            "accept_rate_median_rank0": float(np.median(fr.accept_rate))}
+    out = {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points, construct {construct.name}, "
+                       f"{hi - lo} chains on rank 0, {n_steps} steps"
+                       + ("" if n_steps >= 200000 else " (bounded sample of the configured 200k)"),
+           "n_steps": n_steps, "engine": engine, "chains": int(reduce(len(fr.MCMCresults), "sum")), "device_s": dev_s,
+           "wall_s": wall, "ssfun_evals": evals, "value": evals / wall, "unit": "SS evals/s (wall time)",
+           "scaling": "strong", "us_per_step": wall * 1e6 / max(n_steps - 1, 1),
+           "device_value": evals / dev_s, "device_us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
+           "accept_rate_median_rank0": float(np.median(fr.accept_rate)),
+           "outputs_finite_rank0": ok}
+    spot = {"cells": cells, "construct": construct, "theta": s_theta, "cid": s_cid, "ss_gpu": s_ss}
+    return out, spot
+
+
+def cpu_baseline_synth(cfg: int, spot: dict, seconds: float):
+    """cpu_baseline leg on a BASELINE config-4/5 workload (BASELINE.md CPU plan): the C
+    oracle on the host cores (all threads, then 1 core) over a sample of the 10,000-chain fit's final
+    states (one row per sampled chain), which doubles as the oracle spot check of that fit's
+    outputs: the GPU SS of the same rows (synthetic_end_to_end) against the oracle's."""
+    from oracle import c_oracle  # cpu_baseline leg only
+
+    c_oracle.build()
+    cells, cs = spot["cells"], spot["construct"]
+    th, ci = spot["theta"], spot["cid"]
+    ac = np.ones(len(ci), np.uint8)
+    threads = c_oracle.max_threads()
+    want, st = c_oracle.ss_batch(cells.offsets, cells.t, cells.ms2, cells.pp7, cs, th, ci)
+    rel = float(np.max(np.abs(spot["ss_gpu"] - want) / np.abs(want))) if np.all(st == 0) else float("nan")
+    rate, evals, reps, el = _cpu_rate(cells, cs, th, ci, ac, threads, seconds)
+    one = np.arange(min(len(ci), 64))
+    rate1, evals1, reps1, el1 = _cpu_rate(cells, cs, th[one], ci[one], ac[one], 1, seconds / 2)
+    return {"value": rate, "unit": "SS evals/s", "cores": threads, "kind": "port",
+            "sample": f"config{cfg}: {len(ci)} final chain states of the DRAM fit x {reps} passes = {evals} evals in "
+                      f"{el:.1f} s; C matrix-form oracle, OpenMP {threads} threads",
+            "single_core": {"value": rate1, "unit": "SS evals/s", "cores": 1,
+                            "sample": f"{len(one)} rows x {reps1} passes = {evals1} evals in {el1:.1f} s"},
+            "oracle_spot_check": {"rows": int(len(ci)), "max_rel_err_gpu_vs_oracle": rel,
+                                  "ok": bool(rel <= 1e-6), "tolerance": 1e-6}}
 
 
 def hierarchical_end_to_end(lk, n_steps: int, seed: int, reduce):
@@ -348,8 +391,9 @@ def hierarchical_end_to_end(lk, n_steps: int, seed: int, reduce):
     wall = reduce(time.perf_counter() - t0, "max")
     dev_s, evals = reduce(fr.elapsed_ms * 1e-3, "max"), int(reduce(fr.n_evals, "sum"))
     return {"n_steps": n_steps, "chains": int(reduce(len(fr.MCMCresults), "sum")), "device_s": dev_s, "wall_s": wall,
-            "ssfun_evals": evals, "value": evals / dev_s, "unit": "SS evals/s",
-            "us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
+            "ssfun_evals": evals, "value": evals / wall, "unit": "SS evals/s (wall time)",
+            "us_per_step": wall * 1e6 / max(n_steps - 1, 1),
+            "device_value": evals / dev_s, "device_us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
             "v_fixed": bool(all(abs(r["mean_v"] - v0[int(r["cell_index"]) - 1]) <= 1e-5 + 1e-12
                                 for r in fr.MCMCresults))}
 
@@ -404,6 +448,49 @@ def kernel_sweep(lk, cells, dev, stream, seed: int, Ks=(1, 64, 256, 1024), targe
                     "algorithmic_bytes_per_launch": alg, "achieved_GBs": ach, "hbm_frac": ach / HBM_PEAK_GBS})
         del rounds
     return out
+
+
+def x0_theta_kernel(lk, cells, dev, stream, K: int = 256, seed: int = 1, target_s: float = 0.1):
+    """SURVEY §8(d)(6) kernel-mode theta set: every row drawn from the reference's initial-state
+    distribution (TranscriptionCycleMCMC.m:200-210: v ~ 1+2U, ton ~ 4U, A ~ U, tau ~ 4U, MS2_basal 10,
+    PP7_basal 5, R 15, dR ~ N(0, 3)), numpy seed 1, K rows per cell (all inside the box, so all
+    counted). The same kernel as `value`; only the theta distribution differs."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    C, lens = cells.n_cells, cells.lengths.astype(np.int64)
+    ld = int(7 + lens.max())
+    theta = np.zeros((C * K, ld))
+    for c in range(C):
+        n = int(lens[c])
+        u = rng.random((K, 4))
+        blk = theta[c * K:(c + 1) * K]
+        blk[:, 0], blk[:, 2], blk[:, 5], blk[:, 1] = 1 + 2 * u[:, 0], 4 * u[:, 1], u[:, 2], 4 * u[:, 3]
+        blk[:, 3], blk[:, 4], blk[:, 6] = 10.0, 5.0, 15.0
+        blk[:, 7:7 + n] = rng.normal(0.0, 3.0, (K, n))
+    cid = np.repeat(np.arange(C, dtype=np.int32), K)
+    act = np.ones(C * K, np.uint8)
+    th_d, cid_d = torch.from_numpy(theta).to(dev), torch.from_numpy(cid).to(dev)
+    act_d, out_d = torch.from_numpy(act).to(dev), torch.empty(C * K, dtype=torch.float64, device=dev)
+    for _ in range(8):
+        lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=stream)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 64
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(n):
+        lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / n
+    ss = out_d.cpu().numpy()
+    alg = algorithmic_bytes(cells, cid, act)
+    return {"workload": f"TestData-299cells-x{K}-x0-distribution-theta (seed {seed})", "rows_per_launch": C * K,
+            "in_bounds_per_launch": C * K, "kernel_us": ms * 1e3, "value": C * K * n / wall, "unit": "SS evals/s",
+            "kernel_evals_per_s": C * K / (ms * 1e-3), "algorithmic_bytes_per_launch": alg,
+            "hbm_frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "results_finite": bool(np.all(np.isfinite(ss)))}
 
 
 def drop_in_latency(lk, cells, theta, cid, calls: int = 2000):
@@ -536,7 +623,9 @@ def main():
             "in_bounds_evals_per_launch_per_gpu": float(np.mean(rounds.n_active)),
             "timed_region_s": elapsed,
             "construct": CONSTRUCT,
-            "parallelism": f"replica-per-gpu x{world} (cells independent; 1 RCCL gather after timing)",
+            "parallelism": f"replica-per-gpu x{world} (cells independent" + (
+                f"; 1 {'RCCL' if backend == 'nccl' else 'gloo'} gather after timing)" if distributed else ")"),
+            "launcher": os.environ.get("TCI_BENCH_LAUNCHER") or ("torch.distributed.run" if distributed else "none"),
             "kernel_rows_per_lane": lk.info["rows_per_lane"],
         },
         "roofline": {
@@ -556,6 +645,7 @@ def main():
     }
     if not args.no_sweep:
         res["kernel_sweep"] = kernel_sweep(lk, cells, dev, stream, seed=77 + rank)
+        res["kernel_x0_theta"] = x0_theta_kernel(lk, cells, dev, stream)
     theta_h = rounds.theta[0].cpu().numpy()
     act_h = rounds.active[0].cpu().numpy()
     if rank == 0 and world == 1 and not args.no_latency:
@@ -579,15 +669,18 @@ def main():
         res["end_to_end_dram"] = e2e
         if not args.no_configs:
             res["config3_hierarchical_dram"] = hierarchical_end_to_end(lk, args.dram_steps, seed=3 + rank, reduce=reduce)
+    spots = {}
     if not args.no_configs:
         for cfg in (4, 5):
             res[f"config{cfg}_kernel"] = synthetic_kernel(cfg, rank, world, device_index, 8, args.warmup,
                                                           max(args.steps, 20), reduce)
             if args.synth_dram_steps > 1:
-                res[f"config{cfg}_dram"] = synthetic_end_to_end(cfg, rank, world, device_index, args.synth_dram_steps,
-                                                                reduce)
+                res[f"config{cfg}_dram"], spots[cfg] = synthetic_end_to_end(cfg, rank, world, device_index,
+                                                                            args.synth_dram_steps, reduce)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cells, theta_h, rounds_cid(cells, args.proposals), act_h, args.cpu_seconds)
+        for cfg, spot in spots.items():
+            res[f"cpu_baseline_config{cfg}"] = cpu_baseline_synth(cfg, spot, args.cpu_seconds / 2)
     if rank == 0:
         print(json.dumps(res), flush=True)
     lk.close()
@@ -600,5 +693,86 @@ def rounds_cid(cells, K: int) -> np.ndarray:
     return np.repeat(np.arange(cells.n_cells, dtype=np.int32), K)
 
 
-if __name__ == "__main__":
+# ---------------------------------------------------------------------------
+# --gpus N without a launcher: one child process per GPU (the reference's parfor workers,
+# TranscriptionCycleMCMC.m:161), spawned before anything touches the GPU
+# ---------------------------------------------------------------------------
+
+
+class LaunchError(ValueError):
+    pass
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_plan(gpus: int, env: dict, port: int = 0):
+    """How this invocation runs. None: in this process (a launcher such as torch.distributed.run set
+    WORLD_SIZE, or one GPU). Otherwise one environment per rank for ``gpus`` child processes:
+    RANK = LOCAL_RANK = r, WORLD_SIZE = gpus, rendezvous on 127.0.0.1. An inherited WORLD_SIZE that
+    disagrees with --gpus is an error (LaunchError), never silently the smaller run."""
+    if gpus < 1:
+        raise LaunchError(f"--gpus must be >= 1, got {gpus}")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None and ws != "":
+        if int(ws) != gpus:
+            raise LaunchError(f"--gpus {gpus} disagrees with the launcher's WORLD_SIZE={ws}")
+        return None
+    if gpus == 1:
+        return None
+    port = port or _free_port()
+    return [dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TCI_BENCH_LAUNCHER="bench.py --gpus")
+            for r in range(gpus)]
+
+
+def run_ranks(plan, argv) -> int:
+    """Start one child per rank (this parent never touches the GPU) and wait for all of them. Rank 0
+    prints the JSON line on the inherited stdout. If a rank fails, the others are stopped (their
+    collectives would wait forever) and its exit status is returned."""
+    import subprocess
+
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e) for e in plan]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                r = p.poll()
+                if r is None:
+                    continue
+                procs.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in procs:
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for q in procs:
+            q.kill()
+    return rc
+
+
+def entry() -> int:
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    known, _ = ap.parse_known_args()
+    try:
+        plan = launch_plan(known.gpus, dict(os.environ))
+    except LaunchError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        return 2
+    if plan is not None:
+        return run_ranks(plan, sys.argv[1:])
     main()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(entry())

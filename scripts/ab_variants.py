@@ -14,72 +14,38 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "build", "ab")
 
+# Diagnostics builds (measurement only; the ablations give wrong results on purpose). Any other
+# variant is given ad hoc as NAME=DEF1+DEF2 (e.g. "x=TCI_FOO=1+TCI_BAR=2") for a one-off A/B;
+# rejected experiments are not kept as knobs in the sources (git history has them).
 VARIANTS = {
     "ship": [],
-    "old": None,  # a prebuilt library of the previous commit, copied to build/ab/libtci_old.so
-    "adapt16": ["TCI_ADAPT_WAVES13=16"],
+    "old": None,   # a prebuilt library of the previous commit, copied to build/ab/libtci_old.so
+    "prev": None,  # a prebuilt library of the previous working state
     "abl_rows": ["TCI_ABLATE=1"],
     "abl_interp": ["TCI_ABLATE=4"],
     "abl_scan": ["TCI_ABLATE=8"],
     "abl_all": ["TCI_ABLATE=15"],
-    "w8_latepts": ["TCI_WAVES_PER_EU=8", "TCI_EARLY_POINTS=0"],
     "abl_loads": ["TCI_ABLATE=16"],
     "abl_launch": ["TCI_ABLATE=32"],
-    "wpb1": ["TCI_WAVES_PER_BLOCK=1"],
-    "wpb8": ["TCI_WAVES_PER_BLOCK=8"],
-    "w8": ["TCI_WAVES_PER_EU=8"],
     "chainprof": ["TCI_CHAIN_PROFILE=1"],
     "chainprof2": ["TCI_CHAIN_PROFILE=2"],
-    "rec1_s3": ["TCI_REC_WAVE=1", "TCI_SIG_WAVE=3"],
-    "rec3_s1": ["TCI_REC_WAVE=3", "TCI_SIG_WAVE=1"],
-    "rec1_s2": ["TCI_REC_WAVE=1", "TCI_SIG_WAVE=2"],
-    "rec0_s3": ["TCI_REC_WAVE=0", "TCI_SIG_WAVE=3"],
-    "rec0_s1": ["TCI_REC_WAVE=0", "TCI_SIG_WAVE=1"],
-    "rec2_s0": ["TCI_REC_WAVE=2", "TCI_SIG_WAVE=0"],
-    "normal_f32": ["TCI_NORMAL_F32=1"],
-    "normal_f64": ["TCI_NORMAL_F32=0"],
-    "r02a": None,  # a prebuilt library of commit 8540df6
-    "prev": None,  # a prebuilt library of the previous working state
     "adaptprof": ["TCI_ADAPT_PROFILE=1"],
-    "adapt_twice": ["TCI_ADAPT_TWICE=1"],
     "adapt_nochol": ["TCI_ADAPT_ABLATE=1"],
     "adapt_nocov": ["TCI_ADAPT_ABLATE=2"],
     "draws_nonorm": ["TCI_DRAWS_ABLATE=1"],
     "draws_nomfma": ["TCI_DRAWS_ABLATE=2"],
     "draws_noscal": ["TCI_DRAWS_ABLATE=4"],
     "draws_noR": ["TCI_DRAWS_ABLATE=8"],
-    "draws_p4": ["TCI_DRAW_PASSES=4"],
-    "draws_p7": ["TCI_DRAW_PASSES=7"],
-    "draws_p1": ["TCI_DRAW_PASSES=1"],
-    "launder0": ["TCI_LOOP_LAUNDER=0"],
-    "launder1": ["TCI_LOOP_LAUNDER=1"],
-    "drawsflat": ["TCI_DRAWS_FLAT=1"],
-    "gt1": ["TCI_GT_BATCH=1"],
-    "gt4": ["TCI_GT_BATCH=4"],
-    "gtper1": ["TCI_GT_PER=1"],
-    "gtper4": ["TCI_GT_PER=4"],
-    "gtmg2": ["TCI_GT_MG=2"],
-    "grp2": ["TCI_DRAW_PASSES_GR=2"],
-    "grp7": ["TCI_DRAW_PASSES_GR=7"],
-    "glds0": ["TCI_DRAWS_GLDS=0"],
-    "pf0": ["TCI_DRAWS_PF=0"],
-    "gtp1": ["TCI_GT_PANELS=1"],
-    "gtp3": ["TCI_GT_PANELS=3"],
-    "gtp4": ["TCI_GT_PANELS=4"],
-    "gtp4w3": ["TCI_GT_PANELS=4", "TCI_GT_WPE=3"],
-    "gtp3w3": ["TCI_GT_PANELS=3", "TCI_GT_WPE=3"],
-    "gtt10p4": ["TCI_GT_TILES=10", "TCI_GT_PER=4"],
-    "gtt10": ["TCI_GT_TILES=10"],
-    "gtdirect": ["TCI_GT_DIRECT=1"],
-    "wp4": ["TCI_DRAW_PASSES_WALK=4"],
-    "wp7": ["TCI_DRAW_PASSES_WALK=7"],
-    "gtw16t5": ["TCI_GT_WAVES=16", "TCI_GT_TILES=5"],
-    "gtw16t8": ["TCI_GT_WAVES=16", "TCI_GT_TILES=8"],
-    "gtw16t10": ["TCI_GT_WAVES=16", "TCI_GT_TILES=10"],
-    "pf1": ["TCI_DRAWS_PF=1"],
-    "pf2": ["TCI_DRAWS_PF=2"],
-    "pf5": ["TCI_DRAWS_PF=5"],
 }
+
+
+def parse_variant(spec):
+    """'name' (a table entry) or 'name=DEF1+DEF2' (ad hoc) -> name; registers ad hoc defines."""
+    if "=" in spec:
+        name, defs = spec.split("=", 1)
+        VARIANTS[name] = defs.split("+")
+        return name
+    return spec
 
 
 def build(names, jobs=4):
@@ -144,12 +110,12 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--run", action="store_true")
-    ap.add_argument("--variants", default="ship,abl_rows,abl_bounds,abl_interp,abl_scan,abl_all")
+    ap.add_argument("--variants", default="ship,abl_rows,abl_interp,abl_scan,abl_all")
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--proposals", type=int, default=256)
     a = ap.parse_args()
-    names = a.variants.split(",")
+    names = [parse_variant(v) for v in a.variants.split(",")]
     if a.build:
         build(names)
     if a.run:

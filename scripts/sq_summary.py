@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-wave means of the SQ counters collected by scripts/sq_stalls.sh, per library variant
+"""Per-wave means of the SQ counters collected by rocprofv3 --pmc SQ_ passes, per library variant
 (dispatches alternate between variants in ab_variants.py order)."""
 import collections
 import csv

@@ -1,0 +1,61 @@
+"""bench.py's own multi-GPU launch (`--gpus N` without torch.distributed.run): the launch plan, the
+WORLD_SIZE mismatch exit and the child processes, on CPU (no GPU call is made by any of these)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def _env(**kw):
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    e.update(kw)
+    return e
+
+
+def test_launch_plan_one_gpu_runs_in_process():
+    assert bench.launch_plan(1, _env()) is None
+
+
+def test_launch_plan_spawns_one_rank_per_gpu():
+    plan = bench.launch_plan(4, _env(), port=29517)
+    assert [p["RANK"] for p in plan] == ["0", "1", "2", "3"]
+    assert [p["LOCAL_RANK"] for p in plan] == ["0", "1", "2", "3"]
+    assert all(p["WORLD_SIZE"] == "4" and p["MASTER_ADDR"] == "127.0.0.1" and p["MASTER_PORT"] == "29517"
+               for p in plan)
+
+
+def test_launch_plan_defers_to_a_matching_launcher():
+    assert bench.launch_plan(8, _env(WORLD_SIZE="8", RANK="3", LOCAL_RANK="3")) is None
+
+
+@pytest.mark.parametrize("gpus,ws", [(8, "1"), (2, "4"), (1, "2")])
+def test_launch_plan_rejects_a_mismatched_world(gpus, ws):
+    with pytest.raises(bench.LaunchError):
+        bench.launch_plan(gpus, _env(WORLD_SIZE=ws))
+
+
+def test_mismatch_exits_nonzero_before_any_gpu_work():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=_env(WORLD_SIZE="3"),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2
+    assert "disagrees" in r.stderr
+
+
+def test_spawned_ranks_run_and_exit_cleanly():
+    # every child gets WORLD_SIZE=2, so it runs main() itself: --help exits 0 before touching torch
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--help"], env=_env(),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.count("usage:") == 2
+
+
+def test_a_failing_rank_fails_the_launch():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-such-flag"], env=_env(),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0

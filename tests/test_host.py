@@ -293,6 +293,10 @@ def test_cell_weights_follow_rows_times_window(cells):
         assert w[c] == pytest.approx(n * min((6.626 + 2.0 * 2.0) / (2.0 * d), n))
     wv = cell_weights(cells, v0={1: 4.0})   # a faster previous rate: shorter window
     assert wv[0] < w[0] and np.all(wv[1:] == w[1:])
+    # the round-1 signature (an array of point counts) still works: weights N_c
+    np.testing.assert_array_equal(cell_weights(cells.lengths), cells.lengths.astype(np.float64))
+    with pytest.raises(ValueError):
+        cell_weights(cells, v0=[2.0] * 10)   # a sequence must cover every cell
 
 
 def test_cell_setup_matches_reference_initialisation():

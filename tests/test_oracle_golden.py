@@ -109,6 +109,52 @@ def test_position_matrix_shape_and_forward_accumulation():
     np.testing.assert_array_equal(x[3], [2.5, 1.5, 1.5, 1.5, 0, 0])
 
 
+def test_counter_never_passes_the_column_count():
+    """MATLAB errors ("Index exceeds matrix dimensions", ConstantElongationSim.m:61-64) if
+    floor(counter) > n = floor(sum(R.*dt)) (:47). With sum taken left to right -- the oracle's
+    restatement of :47 -- that cannot happen: the products are >= 0 and rounding is monotone, so
+    every partial sum of ALL steps is >= the ton-gated counter after the same step.
+    Checked here on adversarial sequences: tiny leading terms that the gate removes, terms that
+    accumulate to just below / above integers (0.1 steps), huge-then-tiny mixes."""
+    rng = np.random.default_rng(47)
+    for trial in range(4000):
+        m = int(rng.integers(2, 200))
+        kind = trial % 4
+        if kind == 0:
+            p = np.full(m, 0.1)
+        elif kind == 1:
+            p = rng.random(m) * 10.0 ** rng.integers(-18, 3, m)
+        elif kind == 2:
+            p = np.where(rng.random(m) < 0.5, 1e-16, rng.random(m) * 3)
+        else:
+            p = rng.integers(0, 4, m) * 0.1 + rng.choice([0.0, 2.0 ** -52, 2.0 ** -50], m)
+        gate = int(rng.integers(0, m))          # steps before `gate` are t(i) < ton
+        s, c = 0.0, 0.0
+        for i in range(m):
+            s = s + p[i]
+            if i >= gate:
+                c = c + p[i]
+            assert s >= c
+        assert np.floor(c) <= np.floor(s)
+
+
+def test_oracle_never_raises_the_index_error(construct, c_oracle):
+    """The same property through the oracle's own check (OR_EIDX = -2, tci_oracle.c): rates that
+    clamp to 0 or to tiny values before the onset, 0.1-min steps, onsets on and between grid points."""
+    n = 121
+    t = np.arange(n) * 0.1
+    off = np.array([0, n])
+    y = np.ones(n)
+    rng = np.random.default_rng(61)
+    rows = []
+    for k in range(400):
+        dR = rng.choice([-15.0, -10.0 + 1e-13, 0.0, 0.5], n) + (rng.random(n) < 0.3) * rng.normal(0, 2, n)
+        rows.append(np.concatenate([[2.0, 1.0, (k % 40) * 0.05, 1.0, 1.0, 0.5, 10.0], np.clip(dR, -30, 30)]))
+    ss, st = c_oracle.ss_batch(off, t, y, y, construct, pack(rows), np.zeros(len(rows), np.int32))
+    assert np.all(st == 0), np.unique(st)
+    assert np.all(np.isfinite(ss))
+
+
 @pytest.mark.parametrize("n", [2, 3, 65, 66, 129, 200])
 def test_oracles_agree_on_random_theta(n, construct, c_oracle):
     rng = np.random.default_rng(n)

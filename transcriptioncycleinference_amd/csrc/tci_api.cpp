@@ -10,7 +10,10 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <new>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -228,6 +231,24 @@ const double kP2P_pp7_end[1] = {5.758};
 const double kP2P_pp7_loopn[1] = {24};
 
 }  // namespace
+
+namespace tci {
+
+int ensure_dyn_lds(const void* func, size_t bytes) {
+  if (bytes <= 48 * 1024) return TCI_OK;  // within the default limit
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return TCI_EHIP;
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, size_t> set;  // per device and kernel
+  std::lock_guard<std::mutex> lock(mu);
+  size_t& have = set[{dev, func}];
+  if (bytes <= have) return TCI_OK;
+  if (hipFuncSetAttribute(func, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) return TCI_EHIP;
+  have = bytes;
+  return TCI_OK;
+}
+
+}  // namespace tci
 
 extern "C" {
 

@@ -78,39 +78,21 @@ __device__ __forceinline__ double u01(uint32_t a, uint32_t b) {
   return ((double)x + 0.5) * 0x1p-53;
 }
 
-// Standard normals of the stream (chain, step, purpose), kNPer per Philox call (item), Box-Muller.
-//   f64 (shipped): two 53-bit uniforms per pair, log / sincospi in FP64, 2 normals per call: the
-//     double-precision N(0,1) of mcmcstat's randn (no 2^-24 discretisation, no tail cut).
-//   f32 (TCI_NORMAL_F32=1, A/B only): two 24-bit uniforms per pair, OCML logf / sincospif, 4 per
-//     call; z discretised at 2^-24 with the tails cut at 5.9 sd. Measured 5-7 % faster fits
-//     (profiles/r02_likelihood/r02k_dram_libs.jsonl), not worth the narrower proposals.
-#ifndef TCI_NORMAL_F32
-#define TCI_NORMAL_F32 0
-#endif
-constexpr int kNPer = TCI_NORMAL_F32 ? 4 : 2;
+// Standard normals of the stream (chain, step, purpose), kNPer per Philox call (item), Box-Muller:
+// two 53-bit uniforms per pair, log / sincospi in FP64, 2 normals per call -- the double-precision
+// N(0,1) of mcmcstat's randn (no 2^-24 discretisation, no tail cut). (An fp32 Box-Muller measured
+// 5-7 % faster fits, profiles/r02_likelihood/r02k_dram_libs.jsonl; not worth the narrower proposals.)
+constexpr int kNPer = 2;
 
 __device__ __forceinline__ void normals_at(uint64_t seed, int64_t c, int64_t step, uint32_t purpose, int item,
                                            double (&z)[kNPer]) {
   const uint4 r = rng(seed, c, step, purpose, (uint32_t)item);
-#if TCI_NORMAL_F32
-  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const float u1 = ((float)(w[2 * h] >> 8) + 0.5f) * 0x1p-24f, u2 = (float)(w[2 * h + 1] >> 8) * 0x1p-24f;
-    const float rad = sqrtf(-2.0f * logf(u1));
-    float sn, cs;
-    sincospif(2.0f * u2, &sn, &cs);
-    z[2 * h] = (double)(rad * cs);
-    z[2 * h + 1] = (double)(rad * sn);
-  }
-#else
   const double u1 = u01(r.x, r.y), u2 = u01(r.z, r.w);
   const double rad = sqrt(-2.0 * log(u1));
   double sn, cs;
   sincospi(2.0 * u2, &sn, &cs);  // one reduction for both, exact in units of pi
   z[0] = rad * cs;
   z[1] = rad * sn;
-#endif
 }
 
 // z[0..P) of stream `purpose` into LDS, one Philox call per thread and round.
@@ -683,30 +665,16 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
   }
 }
 
-#ifndef TCI_DRAWS_GLDS
-#define TCI_DRAWS_GLDS 1  // stage R by LDS-DMA (load_R_glds); 0 = through registers (A/B)
-#endif
-#ifndef TCI_DRAWS_PF
-#define TCI_DRAWS_PF 2  // R from global memory: R values prefetched this many k-steps ahead (mfma_zr PF); 0 = off
-#endif
-#ifndef TCI_DRAWS_FLAT
-#define TCI_DRAWS_FLAT 0  // A/B only: 1 = one z*R call through a selected (generic) R pointer
-#endif
 #ifndef TCI_DRAWS_ABLATE
 #define TCI_DRAWS_ABLATE 0  // diagnostics only (wrong results): bit0 no normals, bit1 no MFMA, bit2 no scalars, bit3 no R load
 #endif
+constexpr int kDrawsPF = 2;               // R from global memory: R values prefetched this many k-steps ahead (mfma_zr PF)
 constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each)
 constexpr int kDrawSteps = 8 * kDrawMT;   // steps per pass (2 rows per step)
-#ifndef TCI_DRAW_PASSES
-#define TCI_DRAW_PASSES 2
-#endif
-constexpr int kDrawPasses = TCI_DRAW_PASSES;  // passes per k_draws workgroup (32 steps)
-#ifndef TCI_DRAW_PASSES_GR
-#define TCI_DRAW_PASSES_GR 4
-#endif
+constexpr int kDrawPasses = 2;            // passes per k_draws workgroup (32 steps)
 // passes per workgroup when R is read from global memory (past the LDS budget): every workgroup
 // reads the chain's whole R once per pass, so fewer, longer workgroups read it fewer times
-constexpr int kDrawPassesGR = TCI_DRAW_PASSES_GR;
+constexpr int kDrawPassesGR = 4;
 enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
 
 // Dynamic LDS of k_draws: one pass's normals (2 x kDrawSteps rows of stride L) and the chain's R
@@ -719,12 +687,9 @@ __host__ __device__ inline bool draws_r_lds(int64_t L) {
 __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
   return (2 * kDrawSteps * L) * 8 + (draws_r_lds(L) ? dram_tri_stride(L) * 4 : 0) + 16;
 }
-#ifndef TCI_DRAW_PASSES_WALK
-#define TCI_DRAW_PASSES_WALK 4
-#endif
 // WALK (thousands of chains, one draws workgroup per CU): passes per workgroup with R in LDS,
 // so R is staged once per 64 steps (configs 4/5: 174.3 -> 171.6 us per step; 7 passes: 171.9)
-constexpr int kDrawPassesWalk = TCI_DRAW_PASSES_WALK;
+constexpr int kDrawPassesWalk = 4;
 __host__ __device__ inline int draws_passes(int64_t ld, bool walk) {
   return !draws_r_lds(ld) ? kDrawPassesGR : walk ? kDrawPassesWalk : kDrawPasses;
 }
@@ -751,11 +716,7 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
   double* Z = dyn;
   float* Rl = reinterpret_cast<float*>(Z + 2 * kDrawSteps * L);
   const bool rl = draws_r_lds(ld);
-#if TCI_DRAWS_GLDS
   if (rl && !(TCI_DRAWS_ABLATE & 8)) load_R_glds<kDrawThreads>(Rl, st, c, P);
-#else
-  if (rl && !(TCI_DRAWS_ABLATE & 8)) load_R_f32<kDrawThreads>(Rl, st, c, P);
-#endif
   const float* Rg = st.Rf + c * tri_stride(ld);
   const double a = 0.5 * (double)st.nobs[c];
   const double inv_ds = 1.0 / p.drscale;
@@ -765,6 +726,11 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
     if (step0 > s_end) break;  // uniform over the workgroup
     const int ns = (int)min<int64_t>(kDrawSteps, s_end - step0 + 1);
     if (!(TCI_DRAWS_ABLATE & 1)) draw_block_normals<kDrawThreads>(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
+    // The first pass also waits for R: an LDS-DMA copy is counted on vmcnt, and a workgroup-scope
+    // barrier need not drain vmcnt, so every wave waits for its own pieces explicitly before the
+    // barrier (as composable_kernel's block_sync_lds_direct_load does). Later passes have no DMA in
+    // flight, only the previous pass's global stores, which they must not wait for.
+    if (pass == 0 && rl) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // (the first pass: also R)
     // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
     double* d0 = drow + step0 * DW;
@@ -774,12 +740,8 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
     const auto put = [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; };
     if (!(TCI_DRAWS_ABLATE & 2))
       for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT) {
-#if TCI_DRAWS_FLAT
-        mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, rl ? (const float*)Rl : Rg, P, top, put);
-#else
         if (rl) mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rl, P, top, put);
-        else mfma_zr<kDrawMT, kDrawCT, kDrawWaves, decltype(put), TCI_DRAWS_PF>(Z, L, 2 * ns, Rg, P, top, put);
-#endif
+        else mfma_zr<kDrawMT, kDrawCT, kDrawWaves, decltype(put), kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
       }
     for (int k = w; k < ns; k += kDrawWaves) {
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
@@ -900,21 +862,12 @@ __device__ __forceinline__ uint64_t stamp() {
 //   kRecWave: window row + column sums + posterior Welford + thinned rows of the decided rows;
 //   kSigWave: the sigma2 chain (s2 of each decided row, its statistics and thinned rows) and the
 //             precisions 1/s2 the next decisions use.
-#ifndef TCI_REC_WAVE
-#define TCI_REC_WAVE 0
-#endif
-#ifndef TCI_SIG_WAVE
-#define TCI_SIG_WAVE 2
-#endif
-constexpr int kRecWave = TCI_REC_WAVE, kSigWave = TCI_SIG_WAVE;
-// k_chain / k_walk loop heads: the lane index is re-laundered every round/step, so the 64-bit lane
-// masks derived from it are recomputed (one compare each) instead of living in scalar pairs
-// across the loop. Register allocation only (same bits): it removes k_walk's VGPR spill at RPL = 4
-// (config 5: 199.7 -> 191-193 us per step) and trims the SGPR spill (k_chain<2,1>: 171 -> 126
-// dwords, which measured no faster: the reloads are off the critical path). 0 = off (A/B).
-#ifndef TCI_LOOP_LAUNDER
-#define TCI_LOOP_LAUNDER 1
-#endif
+constexpr int kRecWave = 0, kSigWave = 2;  // (six placements measured within 1 %: r02u_record_wave_placement)
+// k_chain / k_walk loop heads: the lane index is re-laundered every round/step (launder_lane), so
+// the 64-bit lane masks derived from it are recomputed (one compare each) instead of living in
+// scalar pairs across the loop. Register allocation only (same bits): it removes k_walk's VGPR
+// spill at RPL = 4 (config 5: 199.7 -> 191-193 us per step) and trims k_chain<2,1>'s SGPR spill.
+__device__ __forceinline__ void launder_lane(int& lane) { asm volatile("" : "+v"(lane)); }
 
 template <int RPL, int NSEG>
 __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
@@ -1032,9 +985,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 #define TCI_PHASE(k) \
   if (TCI_CHAIN_PROFILE) { t1 = stamp(); ph[k] += t1 - t0; t0 = t1; }
   for (int64_t s = s_begin; s <= s_end; par ^= 1) {
-#if TCI_LOOP_LAUNDER
-    asm volatile("" : "+v"(lane));
-#endif
+    launder_lane(lane);
     const bool has_next = s + 1 <= s_end;
     // the scalar draws of steps s and s+1 (loaded by the previous round; dsc lane sbase + 4 h + slot)
     // are broadcast where they are used, so no scalar copy lives across the evaluation
@@ -1223,16 +1174,9 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 // workgroup barriers; 4 chains per 256-thread workgroup, so a CU holds 4x the chains k_chain's
 // one-workgroup-per-chain layout does. Every value is computed by the same expressions as
 // k_chain (its step-s lanes) and the batched engine: identical chains (tests/test_dram_gpu.py).
-#ifndef TCI_WALK_WAVES
-#define TCI_WALK_WAVES 2  // amdgpu_waves_per_eu register budget of k_walk (0: none; A/B in DESIGN.md §7)
-#endif
-#if TCI_WALK_WAVES > 0
-#define TCI_WALK_OCC __attribute__((amdgpu_waves_per_eu(TCI_WALK_WAVES)))
-#else
-#define TCI_WALK_OCC
-#endif
+// Register budget: two waves per SIMD (229 -> 188 us per config-4 step).
 template <int RPL, int NSEG>
-__global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, DramParams p, KParams kp, int64_t s_begin,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_walk(DramState st, DramParams p, KParams kp, int64_t s_begin,
                                                                 int64_t s_end) {
   constexpr int NJ = RPL + 1;
   constexpr int EV = eval_lds_doubles<RPL>();
@@ -1333,9 +1277,7 @@ __global__ __launch_bounds__(kThreads) TCI_WALK_OCC void k_walk(DramState st, Dr
     for (int k = 0; k < NJ; ++k) u[k] = lane + 64 * k < P ? src[lane + 64 * k] : 0.0;
   };
   for (int64_t s = s_begin; s <= s_end; ++s) {
-#if TCI_LOOP_LAUNDER
-    asm volatile("" : "+v"(lane));
-#endif
+    launder_lane(lane);
     double u[NJ];
     load_u(u, s, 0);
     const double* sc = drow + s * DW + 2 * ld;
@@ -1415,9 +1357,7 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
   const int ct = draws_ct(st.ld, p.walk ? 8 : 4);
   auto kd = p.walk ? (ct <= 2 ? k_draws<8, 2> : k_draws<8, 3>)
                    : (ct <= 2 ? k_draws<4, 2> : ct <= 3 ? k_draws<4, 3> : k_draws<4, 5>);
-  if (lds > 48 * 1024 &&
-      hipFuncSetAttribute((const void*)kd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return TCI_EHIP;
+  if (ensure_dyn_lds((const void*)kd, lds) != TCI_OK) return TCI_EHIP;
   const int npass = draws_passes(st.ld, p.walk != 0);
   const int64_t per_wg = (int64_t)kDrawSteps * npass;  // <= the workgroup's threads (scalar draws)
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
@@ -1791,38 +1731,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8
 //     was positive (a singular matrix keeps the previous R, as mcmcstat).
 // The tile arithmetic is k_adapt_mfma's, so both kernels give the same R up to the order of the
 // scatter's k-steps (rows in batches here).
-#ifndef TCI_GT_TILES
-#define TCI_GT_TILES 8
-#endif
-#ifndef TCI_GT_WAVES
-#define TCI_GT_WAVES 8
-#endif
-constexpr int kGtWaves = TCI_GT_WAVES, kGtTiles = TCI_GT_TILES;
-#ifndef TCI_GT_BATCH
-#define TCI_GT_BATCH 2
-#endif
-constexpr int kGtBatch = TCI_GT_BATCH;  // trailing / R-store tiles whose loads are issued together
-#ifndef TCI_GT_PER
-#define TCI_GT_PER 8
-#endif
-constexpr int kGtPer = TCI_GT_PER;  // window loads in flight per thread
-#ifndef TCI_GT_MG
-#define TCI_GT_MG 1
-#endif
-#ifndef TCI_GT_PANELS
-#define TCI_GT_PANELS 3
-#endif
-#ifndef TCI_GT_WPE
-#define TCI_GT_WPE 4
-#endif
-#ifndef TCI_GT_DIRECT
-#define TCI_GT_DIRECT 0
-#endif
-constexpr int kGtPanels = TCI_GT_PANELS;  // Cholesky panels per trailing pass (1 .. 4)
-// 1: the scatter writes only cov; each tile's first touch in the Cholesky (panel group 0) reads
-// cov + qcovadj I from it, so the tile grid is not written and re-read once (same bits)
-constexpr bool kGtDirect = TCI_GT_DIRECT != 0;
-constexpr int kGtMG = TCI_GT_MG;  // merge group: tiles whose old covariance values are read together
+constexpr int kGtWaves = 8, kGtTiles = 8;  // waves per chain; scatter tiles per wave and pass
+constexpr int kGtBatch = 2;   // trailing / R-store tiles whose loads are issued together
+constexpr int kGtPer = 8;     // window loads in flight per thread
+constexpr int kGtPanels = 3;  // Cholesky panels per trailing pass (1 .. 4; 4 spill at the 128-VGPR budget)
 __host__ __device__ inline int64_t gt_lt(int64_t ld) { return (ld + 15) / 16 * 16; }  // tile-grid side
 __host__ __device__ inline int gt_rows(int64_t P) {  // window rows per LDS batch
   const int64_t LX = (P + 15) / 16 * 16;
@@ -1844,7 +1756,7 @@ __device__ __forceinline__ void tri_tile(int k, int n, int r0, int& ti, int& tj)
   tj = r0 + i + k;
 }
 
-__global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(TCI_GT_WPE))) void k_adapt_gt(DramState st,
+__global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4))) void k_adapt_gt(DramState st,
                                                                                                     DramParams p) {
   constexpr int NW = kGtWaves, NTH = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) double dyn[];
@@ -1924,22 +1836,16 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
     }
     TCI_GPHASE(0)
 #pragma unroll
-    for (int g0 = 0; g0 < kGtTiles; g0 += kGtMG) {
-      // every old value of a group of tiles before any write (a diagonal tile reads the mirrors of
-      // its own elements; one round trip per group)
-      double oldg[kGtMG][4];
+    for (int g = 0; g < kGtTiles; ++g) {
+      // every old value of the tile before any write (a diagonal tile reads the mirrors of its own
+      // elements)
+      double old[4];
 #pragma unroll
-      for (int h = 0; h < kGtMG; ++h)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int g = g0 + h, i = 16 * ti[g] + kq + 4 * q, j = 16 * tj[g] + row;
-          oldg[h][q] = (val[g] && i < P && j < P && na > 0.0) ? cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i] : 0.0;
-        }
-#pragma unroll
-    for (int h = 0; h < kGtMG; ++h) {
-      const int g = g0 + h;
+      for (int q = 0; q < 4; ++q) {
+        const int i = 16 * ti[g] + kq + 4 * q, j = 16 * tj[g] + row;
+        old[q] = (val[g] && i < P && j < P && na > 0.0) ? cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i] : 0.0;
+      }
       if (!val[g]) continue;  // uniform
-      const double* old = oldg[h];
       double* A = tile(ti[g], tj[g]);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1960,9 +1866,8 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
         } else {
           a = i == j ? 1.0 : 0.0;
         }
-        if (!kGtDirect) A[(kq + 4 * q) * 16 + row] = a;
+        A[(kq + 4 * q) * 16 + row] = a;
       }
-    }
     }
   }
   TCI_GPHASE(1)
@@ -1990,23 +1895,12 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
   //      order: the same bits as one pass per panel, 1/kGtPanels of the trailing tile traffic)
   // (1) + (2): the diagonal tile of panel pk in wave 0's registers, then the panel's row tiles
   //     (pk, tj > pk): U_pk' X = A -> X, one column per lane; false if a pivot failed
-  // element (16 ti + lr, 16 tj + row) of cov + qcovadj I (identity past P): a tile's value before
-  // its first Cholesky touch, read from cov (upper triangle; a diagonal tile's lower half from the
-  // mirror), the value the scatter's merge wrote there
-  auto src = [&](int ti, int tj, int lr) -> double {
-    const int i = 16 * ti + lr, j = 16 * tj + row;
-    if (i < P && j < P) {
-      const double cv = cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i];
-      return cv + (i == j ? p.qcovadj : 0.0);
-    }
-    return i == j ? 1.0 : 0.0;
-  };
   auto factor_panel = [&](int pk) -> bool {
     if (w == 0) {
       double* A = tile(pk, pk);
       double dt[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dt[q] = kGtDirect && pk == 0 ? src(pk, pk, kq + 4 * q) : A[(kq + 4 * q) * 16 + row];
+      for (int q = 0; q < 4; ++q) dt[q] = A[(kq + 4 * q) * 16 + row];
       bool bad = false;
       chol16_step<0>(dt, lane, rdg, bad);
       wave_sync();
@@ -2027,7 +1921,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
       double* A = tile(pk, tj);
       double x[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) x[k] = kGtDirect && pk == 0 ? src(pk, tj, k) : A[k * 16 + row];
+      for (int k = 0; k < 16; ++k) x[k] = A[k * 16 + row];
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         x[k] = x[k] * rdg[k];
@@ -2045,9 +1939,8 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
   //     round-robin over waves, kGtBatch tiles at a time: every load of the batch is issued before
   //     the first store (one memory round trip per batch, not per tile: the stores may alias later
   //     loads)
-  auto trail = [&](auto np_c, auto first_c, int pa, int r0, int r1) {
+  auto trail = [&](auto np_c, int pa, int r0, int r1) {
     constexpr int NP = decltype(np_c)::value;
-    constexpr bool FIRST = decltype(first_c)::value;  // the tiles' first touch: read cov (kGtDirect)
     constexpr int BT = NP <= 2 ? kGtBatch : 1;  // tiles per batch (register budget)
     const int m = NT - r0, Ttr = (r1 - r0) * (2 * m - (r1 - r0) + 1) / 2;  // rows r0 .. r1 - 1 of the triangle
     for (int k0 = w; k0 < Ttr; k0 += NW * BT) {
@@ -2063,7 +1956,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
         Ap[g] = tile(ti, tj);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          acc[g][q] = FIRST ? src(ti, tj, kq + 4 * q) : Ap[g][(kq + 4 * q) * 16 + row];
+          acc[g][q] = Ap[g][(kq + 4 * q) * 16 + row];
 #pragma unroll
         for (int h = 0; h < NP; ++h) {
           const double* Xi = tile(pa + h, ti);
@@ -2093,8 +1986,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(T
   auto trail_n = [&](int np, int pa, int r0, int r1) {  // np panels pa .. pa + np - 1
     if (np <= 0 || r0 >= r1) return;
     const auto go = [&](auto np_c) {
-      if (kGtDirect && pa == 0) trail(np_c, std::true_type{}, pa, r0, r1);
-      else trail(np_c, std::false_type{}, pa, r0, r1);
+      trail(np_c, pa, r0, r1);
     };
     switch (np) {
       case 1: go(std::integral_constant<int, 1>{}); break;
@@ -2151,9 +2043,7 @@ inline dim3 chain_grid(int64_t n) { return dim3((unsigned)n); }
 
 int launch_stage(void (*k)(DramState, DramParams), const DramState& st, const DramParams& p, void* stream) {
   const size_t lds = (size_t)stage_lds_bytes(st.ld);
-  if (lds > 48 * 1024 &&
-      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return TCI_EHIP;
+  if (ensure_dyn_lds((const void*)k, lds) != TCI_OK) return TCI_EHIP;
   hipLaunchKernelGGL(k, chain_grid(st.n_chains), dim3(kThreads), lds, (hipStream_t)stream, st, p);
   return finish();
 }
@@ -2162,13 +2052,8 @@ template <int NW, int MAXT, int OWN>
 int launch_adapt_mfma(const DramState& st, const DramParams& p, void* stream) {
   const size_t bytes = (size_t)adapt_mfma_lds_bytes(p.pmax);
   auto k = k_adapt_mfma<NW, MAXT, OWN>;
-  if (bytes > 48 * 1024 &&
-      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
-    return TCI_EHIP;
+  if (ensure_dyn_lds((const void*)k, bytes) != TCI_OK) return TCI_EHIP;
   hipLaunchKernelGGL(k, chain_grid(st.n_chains), dim3(64 * NW), bytes, (hipStream_t)stream, st, p);
-#ifdef TCI_ADAPT_TWICE  // diagnostics only (wrong results): a second, warm launch of the same kernel
-  hipLaunchKernelGGL(k, chain_grid(st.n_chains), dim3(64 * NW), bytes, (hipStream_t)stream, st, p);
-#endif
   return finish();
 }
 
@@ -2193,18 +2078,10 @@ int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream) 
 }
 int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
   if (p.pmax <= 16 * 9) return launch_adapt_mfma<4, 9, 12>(st, p, stream);
-#ifndef TCI_ADAPT_WAVES13
-#define TCI_ADAPT_WAVES13 8  // waves per chain of the P <= 208 adaptation (16 waves x 6 tiles: A/B, slower)
-#endif
-#if TCI_ADAPT_WAVES13 == 16
-  if (p.pmax <= 16 * 13) return launch_adapt_mfma<16, 13, 6>(st, p, stream);
-#else
+  // P <= 208: 8 waves x 12 tiles (16 waves x 6 tiles measured slower)
   if (p.pmax <= 16 * 13) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
-#endif
   const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax);
-  if (lds > 48 * 1024 &&
-      hipFuncSetAttribute((const void*)k_adapt_gt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return TCI_EHIP;
+  if (ensure_dyn_lds((const void*)k_adapt_gt, lds) != TCI_OK) return TCI_EHIP;
   hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.n_chains), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);
   return finish();
 }

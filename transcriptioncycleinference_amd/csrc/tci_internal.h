@@ -1,6 +1,7 @@
 // tci_internal.h -- shared host/device definitions of the MI355X likelihood path.
 #pragma once
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include "tci.h"
@@ -63,6 +64,12 @@ struct KParams {
 };
 
 enum Mode : int { MODE_SS = 0, MODE_FWD_INTERP = 1, MODE_FWD_RAW = 2 };
+
+// Allow `func` up to `bytes` of dynamic LDS (hipFuncAttributeMaxDynamicSharedMemorySize). The
+// attribute is set once per kernel and process, raised only when a larger size is asked for: the
+// DRAM engines launch the same kernels every chunk, and the host call costs a driver round trip.
+// Returns TCI_OK or TCI_EHIP. Thread-safe.
+int ensure_dyn_lds(const void* func, size_t bytes);
 
 // Launch the batched kernel (device pointers). rpl = rows per lane (1,2,4,8); 0 = the long-cell
 // kernel (tci_tile_kernel, any N up to TCI_MAX_POINTS).

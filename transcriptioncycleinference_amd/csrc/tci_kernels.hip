@@ -2,30 +2,17 @@
 // ssfun(theta, cell) evaluation (the algorithm and its exactness arguments: tci_eval.h).
 #include "tci_eval.h"
 
-// Build-time variants for A/B timing (scripts/ab_variants.py); the shipped defaults are below.
-#ifndef TCI_XCD_REMAP
-#define TCI_XCD_REMAP 0      // XCD-aware block -> row-range order (A/B: ~1% slower here; the
-#endif                       // 3.7 MB cell table fits every XCD's L2 anyway)
-#ifndef TCI_WAVES_PER_EU
-#define TCI_WAVES_PER_EU 6   // register budget for 6 waves/SIMD (A/B: 50 us vs 58 us at the
-#endif                       // compiler's default 5 waves; 7-8 waves no faster)
-#ifndef TCI_WAVES_PER_BLOCK
-#define TCI_WAVES_PER_BLOCK 4
-#endif
-#if TCI_WAVES_PER_EU > 0
-#define TCI_OCCUPANCY __attribute__((amdgpu_waves_per_eu(TCI_WAVES_PER_EU)))
-#else
-#define TCI_OCCUPANCY
-#endif
-
 namespace tci {
 
 namespace {
 
-constexpr int kWavesPerBlock = TCI_WAVES_PER_BLOCK;
+// 4 independent waves per 256-thread block (1- and 8-wave blocks measured no faster). Register
+// budget for 6 waves/SIMD: 50 vs 58 us per launch at the compiler's default 5; 7-8 no faster.
+// (An XCD-aware block -> row-range order measured ~1 % slower: the cell table fits every XCD's L2.)
+constexpr int kWavesPerBlock = 4;
 
 template <int RPL, int NSEG, int MODE>
-__global__ __launch_bounds__(64 * TCI_WAVES_PER_BLOCK) TCI_OCCUPANCY void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
+__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(6))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
@@ -35,16 +22,7 @@ __global__ __launch_bounds__(64 * TCI_WAVES_PER_BLOCK) TCI_OCCUPANCY void tci_co
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs; give each XCD a
-  // contiguous range of rows so rows of the same cell share one XCD's L2 (speed only).
-#if TCI_XCD_REMAP
-  const unsigned nb = gridDim.x, bid = blockIdx.x;
-  const unsigned xq = nb / 8, xr = nb % 8, xcd = bid % 8, xk = bid / 8;
-  const unsigned vb = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
-#else
-  const unsigned vb = blockIdx.x;
-#endif
-  const int64_t b = (int64_t)vb * kWavesPerBlock + wid;
+  const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wid;
   if (b >= B) return;
   double* lds = s_lds[wid];
 #if TCI_ABLATE & 32
@@ -373,10 +351,11 @@ __global__ __launch_bounds__(64) void tci_tile_kernel(const KParams kp, const do
 template <int NSEG, int MODE>
 int launch_tile(const KParams& kp, const double* theta, int64_t ld, const int32_t* cell_id, const uint8_t* active,
                 int64_t B, double* out0, double* out1, int64_t ld_out, hipStream_t stream) {
+  // LDS sized by the context's longest cell (64 B per point: 131 KB at 2,048 points, one wave per
+  // CU); the limit is raised once, to the largest cell any context allows (ensure_dyn_lds)
   const size_t lds = (size_t)tile_lds_doubles(kp.max_n) * sizeof(double);
   auto k = tci_tile_kernel<NSEG, MODE>;
-  if (lds > 48 * 1024 &&
-      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+  if (ensure_dyn_lds((const void*)k, (size_t)tile_lds_doubles(TCI_MAX_POINTS) * sizeof(double)) != TCI_OK)
     return TCI_EHIP;
   hipLaunchKernelGGL(k, dim3((unsigned)B), dim3(64), lds, stream, kp, theta, ld, cell_id, active, B, out0, out1, ld_out);
   return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;

@@ -43,9 +43,20 @@ def cell_weights(cells, L0: float = 6.626, v0=None) -> np.ndarray:
     inside the elongation window, W_c = (L0 + tau*v) / (v * d_c) grid steps (capped at N_c) at
     the prior means of v and tau; d_c = mean(diff(t)) is the cell's grid increment
     (SumofSquares...m:29). ``v0`` (hierarchical fit, a mapping by 1-based cell_index or a
-    sequence over all cells) replaces the prior mean of v where given."""
+    sequence over all cells) replaces the prior mean of v where given.
+
+    ``cells`` is a :class:`~.data.Cells`, or (the round-1 signature) an array of the cells'
+    point counts N_c: without times there is no window, and the weights are N_c alone."""
     from .mcmc import PreviousFit, _per_cell
 
+    if not hasattr(cells, "lengths"):
+        lens = np.asarray(cells, dtype=np.float64)
+        if lens.ndim != 1:
+            raise ValueError("cell_weights: expected a Cells table or a 1-D array of point counts")
+        return lens.copy()
+    if v0 is not None and not hasattr(v0, "get") and len(v0) != cells.n_cells:
+        raise ValueError(f"cell_weights: v0 has {len(v0)} entries for {cells.n_cells} cells "
+                         "(a sequence must cover every cell; use a cell_index mapping for a subset)")
     n = cells.lengths.astype(np.float64)
     w = np.empty(cells.n_cells)
     for c in range(cells.n_cells):
