@@ -125,6 +125,11 @@ int tci_ssfun(tci_ctx* ctx, int32_t cell, const double* theta, int64_t P, double
 int tci_forward(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int32_t* cell_id, int64_t B,
                 int grid_mode, double* ms2_out, double* pp7_out, int64_t ld_out);
 
+/* Number of HIP devices visible to this process (*n_out = 0 when there is none; never an error
+ * for that). Lets a caller spread contexts over a node's GPUs, e.g. the reference's parfor worker k
+ * (TranscriptionCycleMCMC.m:161) on device (k - 1) mod n (matlab/tci_ssfun.m). */
+int tci_device_count(int* n_out);
+
 /* Number of acquisition points of a cell, and the grid the SS uses for it (M points). */
 int tci_cell_points(const tci_ctx* ctx, int32_t cell, int64_t* n_out);
 int tci_cell_grid(const tci_ctx* ctx, int32_t cell, double* t_interp_out, int64_t cap, int64_t* m_out);

@@ -6,6 +6,9 @@
 //
 //   mex -R2018a -I../include matlab/tci_mex.cpp -L../transcriptioncycleinference_amd -ltci
 //
+// Here (no MATLAB) it is compiled against the builder-written stand-in API in matlab/mexstub/ and
+// executed by tests/test_mex_gateway.py (transcriptioncycleinference_amd/build.py:build_mex_stub).
+//
 // Commands (handles are uint64 scalars; cells are 1-based as in MATLAB):
 //   h  = tci_mex('create', data, construct, device)
 //          data: struct array with fields time, MS2, PP7 (README.md:11-16), already truncated
@@ -17,6 +20,7 @@
 //   ss = tci_mex('ss_batch', h, cells, X, active)   active: 1 x B logical (false -> +Inf)
 //   [ms2, pp7] = tci_mex('forward', h, cell, x, 'raw' | 'interp')
 //   tci_mex('destroy', h)
+//   n = tci_mex('device_count')                 HIP devices visible to this MATLAB process
 // Errors are raised with mexErrMsgIdAndTxt('tci:...'), carrying tci_last_error().
 // Every argument's class and size is checked before a pointer reaches the C ABI. Live contexts
 // are tracked; a handle that this MEX file did not create (or already destroyed) is rejected,
@@ -133,7 +137,8 @@ void cmd_create(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     if (ctx) tci_destroy(ctx);
     mexErrMsgIdAndTxt("tci:create", "%s", msg.c_str());
   }
-  live().insert(ctx);  plhs[0] = mxCreateNumericMatrix(1, 1, mxUINT64_CLASS, mxREAL);
+  live().insert(ctx);
+  plhs[0] = mxCreateNumericMatrix(1, 1, mxUINT64_CLASS, mxREAL);
   *static_cast<uint64_t*>(mxGetData(plhs[0])) = static_cast<uint64_t>(reinterpret_cast<uintptr_t>(ctx));
   (void)nlhs;
 }
@@ -210,6 +215,11 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   else if (cmd == "ss") cmd_ss(plhs, nrhs, prhs);
   else if (cmd == "ss_batch") cmd_ss_batch(plhs, nrhs, prhs);
   else if (cmd == "forward") cmd_forward(nlhs, plhs, nrhs, prhs);
+  else if (cmd == "device_count") {
+    int n = 0;
+    tci_device_count(&n);
+    plhs[0] = mxCreateDoubleScalar((double)n);
+  }
   else if (cmd == "destroy") {
     if (nrhs > 1) {
       tci_ctx* c = handle_of(prhs[1]);

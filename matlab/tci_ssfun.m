@@ -9,15 +9,21 @@ function SS = tci_ssfun(construct, data, x)
 %   Use it exactly where TranscriptionCycleMCMC.m:186 builds the mcmcstat handle:
 %       ssfun = @(x,data) tci_ssfun(construct,data,x);
 %
-%   A device context is created once per distinct (construct, data) in each MATLAB process
-%   (parfor workers are separate processes and each keep their own) and reused for every
-%   later call with the same data, which is what mcmcstat does. The cache is keyed by a SHA-1
-%   of the exact bytes of [t, y] (as the Python twin ssfun.py does) and a hit is confirmed by
-%   comparing the stored bytes, so two cells never share a context. At most MAX_CTX contexts
-%   are kept; the least recently used one is destroyed beyond that.
-%   TCI_SSFUN() with no arguments destroys every cached context.
+%   construct: a name ('P2P-MS2v5-LacZ-PP7v4') or a struct with fields L0, MS2_start, MS2_end,
+%   MS2_loopn, PP7_start, PP7_end, PP7_loopn (one entry per stem-loop segment).
+%
+%   Device: the parfor over cells (TranscriptionCycleMCMC.m:161) runs each cell in a worker
+%   process; worker k (getCurrentTask().ID) uses GPU mod(k-1, n) of the n GPUs tci_mex sees, so
+%   the workers of an 8-GPU node spread over all 8. Outside a parfor: GPU 0.
+%
+%   Contexts: one per distinct (construct, data) in each MATLAB process, reused for every later
+%   call with the same data -- mcmcstat passes the same data on every call of a chain. The last
+%   context is checked first by a byte compare of [t, y]; other cached ones are found by a cheap
+%   fingerprint (length, end points, sums) and confirmed by the same byte compare, so two cells
+%   never share a context and nothing is hashed per call. At most MAX_CTX contexts are kept; the
+%   least recently used one is destroyed beyond that. TCI_SSFUN() destroys every cached context.
 MAX_CTX = 64;
-persistent cache stamp
+persistent cache stamp last dev
 if isempty(cache)
     cache = containers.Map('KeyType', 'char', 'ValueType', 'any');
     stamp = 0;
@@ -29,22 +35,38 @@ if nargin == 0
         tci_mex('destroy', e.h);
     end
     cache = containers.Map('KeyType', 'char', 'ValueType', 'any');
+    last = [];
     SS = [];
     return
 end
+if isempty(dev)
+    dev = 0;
+    ngpu = tci_mex('device_count');
+    if ngpu > 0 && exist('getCurrentTask', 'file')
+        task = getCurrentTask();          % empty outside a parallel pool
+        if ~isempty(task)
+            dev = mod(task.ID - 1, ngpu);
+        end
+    end
+end
 t = double(data.xdata(:)');
 y = double(data.ydata(:)');
-n = numel(t);
 bytes = typecast([t, y], 'uint8');
-md = java.security.MessageDigest.getInstance('SHA-1');
-md.update(bytes);
-key = [construct, '|', sprintf('%d|', n), sprintf('%02x', typecast(md.digest(), 'uint8'))];
+ckey = construct_key(construct);
+% the common case: the same cell as the previous call (one compare, no map lookup)
+if ~isempty(last) && strcmp(last.ckey, ckey) && isequal(last.bytes, bytes)
+    SS = tci_mex('ss', last.h, 1, x);
+    return
+end
+n = numel(t);
+yf = y(~isnan(y));
+key = sprintf('%s|%d|%.17g|%.17g|%.17g|%.17g', ckey, n, t(1), t(end), sum(t), sum(yf));
 stamp = stamp + 1;
 hit = false;
 if isKey(cache, key)
     e = cache(key);               % containers.Map allows one level of indexing only
     hit = isequal(e.bytes, bytes);
-    if ~hit                       % a SHA-1 collision: never reuse another cell's context
+    if ~hit                       % same fingerprint, other data: never reuse another cell's context
         tci_mex('destroy', e.h);
         remove(cache, key);
     end
@@ -61,10 +83,27 @@ else
         old = cache(ks{i});
         tci_mex('destroy', old.h);
         remove(cache, ks{i});
+        if ~isempty(last) && last.h == old.h
+            last = [];
+        end
     end
     cell_data = struct('time', t, 'MS2', y(1:n), 'PP7', y(n+1:end));
-    e = struct('h', tci_mex('create', cell_data, construct, 0), 'bytes', bytes, 'used', stamp);
+    e = struct('h', tci_mex('create', cell_data, construct, dev), 'bytes', bytes, 'used', stamp);
     cache(key) = e;
 end
+last = struct('h', e.h, 'bytes', bytes, 'ckey', ckey);
 SS = tci_mex('ss', e.h, 1, x);
+end
+
+function k = construct_key(construct)
+% A text key of a construct name or struct (every field's values, full precision).
+if ischar(construct)
+    k = construct;
+else
+    f = {'L0', 'MS2_start', 'MS2_end', 'MS2_loopn', 'PP7_start', 'PP7_end', 'PP7_loopn'};
+    k = '';
+    for i = 1:numel(f)
+        k = [k, f{i}, '=', sprintf('%.17g,', construct.(f{i})), ';']; %#ok<AGROW>
+    end
+end
 end

@@ -1,0 +1,188 @@
+"""The MATLAB MEX gateway (matlab/tci_mex.cpp) executed through the stand-in MATLAB API
+(matlab/mexstub/, MATLAB itself is absent): argument checks and error identifiers on CPU; on the
+GPU the SS / forward results of `tci_mex` against the Python binding of the same C ABI, bit for bit,
+with MATLAB's conventions -- column-major P x B theta, 1-based cells, logical or double `active`.
+The gateway stands in for the reference's ssfun hook (TranscriptionCycleMCMC.m:186,258)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, pack
+from mexharness import Mex, MexError, MxPtr
+
+DATA_FIELDS = ["time", "MS2", "PP7", "name"]
+
+
+@pytest.fixture(scope="module")
+def mex():
+    from transcriptioncycleinference_amd.build import MEX_STUB, build_library, build_mex_stub
+
+    build_library()
+    srcs = [os.path.join(ROOT, "matlab", "tci_mex.cpp")] + [
+        os.path.join(ROOT, "matlab", "mexstub", f) for f in ("mex.h", "matrix.h", "mexstub.cpp")]
+    if not os.path.exists(MEX_STUB) or any(os.path.getmtime(s) > os.path.getmtime(MEX_STUB) for s in srcs):
+        build_mex_stub()
+    m = Mex(MEX_STUB)
+    yield m
+    m.clear()
+
+
+def data_struct(mex, cells, ids):
+    rows = []
+    for c in ids:
+        t, m, p = cells.cell(c)
+        rows.append({"time": t, "MS2": m, "PP7": p, "name": "TestData"})
+    return MxPtr(mex, mex.struct(rows, DATA_FIELDS))
+
+
+def expect(ident, fn, *a, **k):
+    with pytest.raises(MexError) as e:
+        fn(*a, **k)
+    assert e.value.ident == ident, (e.value.ident, e.value.msg)
+    return e.value
+
+
+# ---- CPU: everything the gateway checks before a pointer reaches the C ABI -------------------
+
+
+def test_commands_and_handles_are_checked(mex):
+    expect("tci:arg", mex.call, 3.0)                        # first argument must be a command
+    expect("tci:arg", mex.call, "no_such_command")
+    expect("tci:handle", mex.call, "ss", MxPtr(mex, mex.handle(12345)), 1.0, np.zeros(130))
+    expect("tci:handle", mex.call, "ss", 7.0, 1.0, np.zeros(130))   # a double is not a handle
+    expect("tci:handle", mex.call, "destroy", MxPtr(mex, mex.handle(0xdeadbeef)))
+    expect("tci:arg", mex.call, "ss", nlhs=1)              # wrong argument count
+
+
+def test_create_checks_data_and_construct(mex, cells):
+    expect("tci:arg", mex.call, "create")
+    expect("tci:data", mex.call, "create", np.zeros(3), "P2P-MS2v5-LacZ-PP7v4")   # not a struct
+    d = data_struct(mex, cells, [0, 1])
+    try:
+        expect("tci:construct", mex.call, "create", d, "P2P-other")              # GetFluorFromPolPos.m:18
+        expect("tci:construct", mex.call, "create", d, 5.0)
+        bad = MxPtr(mex, mex.struct([{"L0": 6.626, "MS2_start": [0.0, 1.0], "MS2_end": [0.5], "MS2_loopn": [24.0],
+                                      "PP7_start": [4.0], "PP7_end": [5.0], "PP7_loopn": [24.0]}],
+                                    ["L0", "MS2_start", "MS2_end", "MS2_loopn", "PP7_start", "PP7_end", "PP7_loopn"]))
+        expect("tci:construct", mex.call, "create", d, bad)
+        bad.free()
+    finally:
+        d.free()
+    t, m, p = cells.cell(0)
+    ragged = MxPtr(mex, mex.struct([{"time": t, "MS2": m[:-1], "PP7": p}], DATA_FIELDS))
+    expect("tci:data", mex.call, "create", ragged, "P2P-MS2v5-LacZ-PP7v4")      # lengths differ
+    ragged.free()
+    nofield = MxPtr(mex, mex.struct([{"time": t, "MS2": m}], ["time", "MS2"]))
+    expect("tci:data", mex.call, "create", nofield, "P2P-MS2v5-LacZ-PP7v4")     # no PP7
+    nofield.free()
+
+
+def test_device_count_and_create_without_a_gpu(mex, cells):
+    n = mex.call("device_count")[0]
+    assert n.shape == (1, 1) and n[0, 0] >= 0
+    if n[0, 0] == 0:  # this container: the host-side validation passes, the HIP context cannot exist
+        d = data_struct(mex, cells, [0])
+        e = expect("tci:create", mex.call, "create", d, "P2P-MS2v5-LacZ-PP7v4", 0.0)
+        d.free()
+        assert "hip" in e.msg.lower()
+
+
+# ---- GPU: the gateway's results against the Python binding of the same ABI -------------------
+
+
+@pytest.fixture(scope="module")
+def gw(mex, cells):
+    d = data_struct(mex, cells, range(cells.n_cells))
+    h = mex.call("create", d, "P2P-MS2v5-LacZ-PP7v4", 0.0)[0]
+    d.free()
+    yield MxPtr(mex, mex.handle(int(h[0, 0])))
+
+
+@pytest.fixture(scope="module")
+def lk(cells):
+    from transcriptioncycleinference_amd import Likelihood
+
+    with Likelihood(cells, "P2P-MS2v5-LacZ-PP7v4", device=0) as L:
+        yield L
+
+
+@pytest.mark.gpu
+def test_ss_one_based_cells_equals_the_binding(mex, gw, lk, chain, cells):
+    rows = [(int(chain["cell_id"][b]), chain["rows"][b]) for b in range(0, len(chain["rows"]), 37)]
+    want = lk.ss_batch(pack([r for _, r in rows], 136), np.array([c for c, _ in rows], np.int32))
+    got = np.array([mex.call("ss", gw, float(c + 1), r)[0][0, 0] for c, r in rows])   # MATLAB cell c+1
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(got, chain["ss"][::37])                              # the committed goldens
+    expect("tci:arg", mex.call, "ss", gw, 0.0, rows[0][1])        # cells are 1-based
+    expect("tci:arg", mex.call, "ss", gw, 1.5, rows[0][1])
+    expect("tci:call", mex.call, "ss", gw, 300.0, rows[0][1])     # 299 cells: TCI_ERANGE
+    expect("tci:call", mex.call, "ss", gw, 1.0, rows[0][1][:50])  # x shorter than 7 + N
+
+
+@pytest.mark.gpu
+def test_ss_batch_column_major_and_active_masks(mex, gw, lk, chain):
+    B = 300
+    theta = pack(chain["rows"][:B], 136)
+    cid = np.asarray(chain["cell_id"][:B], np.int32)
+    want = lk.ss_batch(theta, cid)
+    X = theta.T                                   # P x B: one theta per COLUMN, as mcmcstat holds them
+    got = mex.call("ss_batch", gw, (cid + 1).astype(np.float64), X)[0]
+    assert got.shape == (B, 1)
+    np.testing.assert_array_equal(got[:, 0], want)
+    act = (np.arange(B) % 3) != 0
+    lg = MxPtr(mex, mex.logical(act))
+    got_l = mex.call("ss_batch", gw, (cid + 1).astype(np.float64), X, lg)[0][:, 0]
+    lg.free()
+    got_d = mex.call("ss_batch", gw, (cid + 1).astype(np.float64), X, act.astype(np.float64) * 2.5)[0][:, 0]
+    for g in (got_l, got_d):
+        np.testing.assert_array_equal(g[act], want[act])
+        assert np.all(np.isposinf(g[~act]))      # skipped proposals
+    expect("tci:arg", mex.call, "ss_batch", gw, (cid[:10] + 1).astype(np.float64), X)   # B mismatch
+    expect("tci:arg", mex.call, "ss_batch", gw, (cid + 1).astype(np.float64), X, act[:5].astype(np.float64))
+    expect("tci:arg", mex.call, "ss_batch", gw, cid.astype(np.float64) + 0.5, X)        # non-integer cells
+
+
+@pytest.mark.gpu
+def test_forward_raw_and_interp(mex, gw, lk, means, cells):
+    for c in (0, 150, 298):
+        x = means["rows"][c]
+        for mode in ("raw", "interp"):
+            ms2, pp7 = mex.call("forward", gw, float(c + 1), x, mode, nlhs=2)
+            wm, wp = lk.forward(x[None, :], np.array([c], np.int32), grid=mode)
+            n = int(cells.lengths[c])
+            assert ms2.shape == (1, n)
+            np.testing.assert_array_equal(ms2[0], wm[0, :n])
+            np.testing.assert_array_equal(pp7[0], wp[0, :n])
+        o, e = cells.offsets[c], cells.offsets[c + 1]
+        raw = mex.call("forward", gw, float(c + 1), x, nlhs=1)[0]      # default 'raw': the plot vectors
+        np.testing.assert_allclose(raw[0], means["sim_ms2"][o:e], rtol=1e-12, atol=0)
+
+
+@pytest.mark.gpu
+def test_custom_construct_struct_and_destroy(mex, cells):
+    from transcriptioncycleinference_amd import Likelihood
+    from transcriptioncycleinference_amd.construct import long_two_loop_construct
+
+    cs = long_two_loop_construct()
+    st = MxPtr(mex, mex.struct([{"L0": cs.L0, "MS2_start": cs.ms2_start, "MS2_end": cs.ms2_end,
+                                 "MS2_loopn": cs.ms2_loopn, "PP7_start": cs.pp7_start, "PP7_end": cs.pp7_end,
+                                 "PP7_loopn": cs.pp7_loopn}],
+                               ["L0", "MS2_start", "MS2_end", "MS2_loopn", "PP7_start", "PP7_end", "PP7_loopn"]))
+    d = data_struct(mex, cells, range(20))
+    h = mex.call("create", d, st, 0.0)[0]
+    d.free()
+    st.free()
+    hp = MxPtr(mex, mex.handle(int(h[0, 0])))
+    rng = np.random.default_rng(5)
+    from transcriptioncycleinference_amd.data import draw_x0
+
+    rows = [draw_x0(rng, int(cells.lengths[c])) for c in range(20)]
+    theta = pack(rows, 136)
+    with Likelihood(cells.subset(range(20)), cs, device=0) as L:
+        want = L.ss_batch(theta, np.arange(20, dtype=np.int32))
+    got = mex.call("ss_batch", hp, np.arange(1, 21, dtype=np.float64), theta.T)[0][:, 0]
+    np.testing.assert_array_equal(got, want)
+    mex.call("destroy", hp, nlhs=0)
+    expect("tci:handle", mex.call, "ss", hp, 1.0, rows[0])   # a destroyed handle is rejected
+    hp.free()

@@ -82,6 +82,7 @@ SIGNATURES = [
                                      C.c_void_p, C.c_void_p]),
     ("tci_ssfun", C.c_int, [C.c_void_p, C.c_int32, _dp, C.c_int64, _dp]),
     ("tci_forward", C.c_int, [C.c_void_p, _dp, C.c_int64, _i32p, C.c_int64, C.c_int, _dp, _dp, C.c_int64]),
+    ("tci_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("tci_cell_points", C.c_int, [C.c_void_p, C.c_int32, _i64p]),
     ("tci_cell_grid", C.c_int, [C.c_void_p, C.c_int32, _dp, C.c_int64, _i64p]),
     ("tci_dram_defaults", C.c_int, [C.POINTER(tci_dram_options)]),

@@ -52,5 +52,26 @@ def build_library(force: bool = False, verbose: bool = False, out: str = LIB, de
     return out
 
 
+MEX_DIR = os.path.join(REPO_ROOT, "matlab")
+MEX_STUB = os.path.join(MEX_DIR, "mexstub", "libtci_mex_stub.so")
+
+
+def build_mex_stub(verbose: bool = False) -> str:
+    """Compile the MATLAB MEX gateway (matlab/tci_mex.cpp) against the builder-written stand-in
+    MATLAB API (matlab/mexstub/: MATLAB's own mex.h is absent here) into one shared library linked
+    to libtci.so, so tests/test_mex_gateway.py can execute mexFunction. Test infrastructure: a MATLAB
+    user builds tci_mex.cpp with `mex`."""
+    stub = os.path.join(MEX_DIR, "mexstub")
+    cxx = shutil.which("g++") or "g++"
+    cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-fPIC", "-shared", "-I" + stub, "-I" + os.path.join(REPO_ROOT, "include"),
+           os.path.join(MEX_DIR, "tci_mex.cpp"), os.path.join(stub, "mexstub.cpp"), "-L" + PKG_DIR, "-ltci",
+           "-Wl,-rpath,$ORIGIN/../../transcriptioncycleinference_amd", "-o", MEX_STUB + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(MEX_STUB + ".tmp", MEX_STUB)
+    return MEX_STUB
+
+
 if __name__ == "__main__":
     print(build_library(force="--force" in sys.argv, verbose=True))

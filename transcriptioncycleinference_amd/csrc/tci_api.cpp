@@ -507,6 +507,14 @@ int tci_forward(tci_ctx* ctx, const double* theta, int64_t ld_theta, const int32
   return TCI_OK;
 }
 
+int tci_device_count(int* n_out) {
+  if (!n_out) return TCI_EINVAL;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;  // hipErrorNoDevice: none visible
+  *n_out = n;
+  return TCI_OK;
+}
+
 int tci_cell_points(const tci_ctx* ctx, int32_t cell, int64_t* n_out) {
   if (!ctx || !n_out || cell < 0 || cell >= ctx->n_cells) return TCI_EINVAL;
   *n_out = ctx->meta[(size_t)cell].n;
