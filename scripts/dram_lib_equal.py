@@ -11,7 +11,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from transcriptioncycleinference_amd import Likelihood, testdata  # noqa: E402
-from transcriptioncycleinference_amd.mcmc import fit  # noqa: E402
+from transcriptioncycleinference_amd.mcmc import DramOptions, fit  # noqa: E402
 
 
 def run(lib, steps, n, cfg):
@@ -21,9 +21,15 @@ def run(lib, steps, n, cfg):
     else:
         import bench
         cells, _, con = bench.synthetic_config_cells(cfg, 0, 1, 0, int(os.environ.get("TCI_SYNTH_POINTS", "200")))[:3]
+    engine = os.environ.get("TCI_ENGINE", "auto")
     with Likelihood(cells, con, lib_path=path) as lk:
-        fr = fit(lk, n_steps=steps, n_burn=steps // 4, seed=3, cells=list(range(n)))
-    return np.array([[r[k] for k in sorted(r) if np.isscalar(r[k]) and isinstance(r[k], float)] for r in fr.MCMCresults])
+        fr = fit(lk, n_steps=steps, n_burn=steps // 4, seed=3, cells=list(range(n)), opts=DramOptions(engine=engine))
+    # every output: the scalar summaries, mean/sigma of dR, the final states, acceptance, evaluations
+    rows = []
+    for k, r in enumerate(fr.MCMCresults):
+        sc = [r[f] for f in sorted(r) if np.isscalar(r[f]) and isinstance(r[f], float)]
+        rows.append(np.concatenate([sc, r["mean_dR"], r["sigma_dR"], fr.final_theta[k], [fr.accept_rate[k]]]))
+    return np.array(rows + [np.full(len(rows[0]), float(fr.n_evals))])
 
 
 a, b = sys.argv[1], sys.argv[2]

@@ -18,6 +18,7 @@ if os.environ.get("TCI_LIB"):  # an A/B build variant (scripts/ab_variants.py) f
 args = sys.argv[1:]
 for i in range(0, len(args), 2):
     cfg, steps = int(args[i]), int(args[i + 1])
-    print(json.dumps(bench.synthetic_end_to_end(cfg, 0, 1, 0, steps, reduce=lambda x, op: x,
-                                                    engine=os.environ.get("TCI_ENGINE", "auto"),
-                                                    n_points=int(os.environ.get("TCI_SYNTH_POINTS", "200")))), flush=True)
+    out, _ = bench.synthetic_end_to_end(cfg, 0, 1, 0, steps, reduce=lambda x, op: x,
+                                        engine=os.environ.get("TCI_ENGINE", "auto"),
+                                        n_points=int(os.environ.get("TCI_SYNTH_POINTS", "200")))
+    print(json.dumps(out), flush=True)

@@ -268,8 +268,8 @@ def test_fused_and_batched_engines_give_identical_chains(lk, ntry):
 def test_adapted_proposal_is_the_scaled_chain_covariance(lk, engine):
     """mcmcstat's adaptation: after the last adaptation row n (n >= burnintime), the proposal
     factor satisfies R'R = (2.4/sqrt(P))^2 (cov(chain rows 1..n) + qcovadj I) with the sample
-    covariance of every row so far (covupd's recurrence); R is kept float-representable
-    (tci_dram.hip header), hence the 1e-6 tolerance."""
+    covariance of every row so far (covupd's recurrence). R is FP64, as mcmcstat's double chol:
+    the factorisation agrees to 1e-12 (round 2 kept R float-representable and needed 1e-6)."""
     from transcriptioncycleinference_amd.mcmc import DramOptions
 
     ids = list(range(0, 299, 37))
@@ -285,10 +285,10 @@ def test_adapted_proposal_is_the_scaled_chain_covariance(lk, engine):
         C = np.cov(X.T, ddof=1) + 1e-5 * np.eye(P)
         R = res.qcov_R[k, :P, :P]
         assert np.all(np.tril(R, -1) == 0)
-        assert np.array_equal(R, R.astype(np.float32).astype(np.float64))
+        assert not np.array_equal(R, R.astype(np.float32).astype(np.float64))  # no fp32 rounding
         Q = R.T @ R
         want = (2.4 ** 2 / P) * C
-        np.testing.assert_allclose(Q, want, rtol=1e-6, atol=1e-6 * np.abs(want).max())
+        np.testing.assert_allclose(Q, want, rtol=1e-12, atol=1e-12 * np.abs(want).max())
 
 
 @pytest.mark.parametrize("engine", ["fused", "batched", "walk"])
@@ -485,9 +485,9 @@ def test_long_cells_adapted_proposal_is_the_scaled_chain_covariance(lk_long, eng
         C = np.cov(X.T, ddof=1) + 1e-5 * np.eye(P)
         R = res.qcov_R[k, :P, :P]
         assert np.all(np.tril(R, -1) == 0)
-        assert np.array_equal(R, R.astype(np.float32).astype(np.float64))
+        assert not np.array_equal(R, R.astype(np.float32).astype(np.float64))  # FP64 R
         want = (2.4 ** 2 / P) * C
-        np.testing.assert_allclose(R.T @ R, want, rtol=1e-6, atol=1e-6 * np.abs(want).max())
+        np.testing.assert_allclose(R.T @ R, want, rtol=1e-12, atol=1e-12 * np.abs(want).max())
     if engine == "batched":
         for other in ("fused", "walk"):
             o.engine = other
@@ -564,4 +564,4 @@ def test_very_long_cells_sample_and_adapt(n):
         R = res.qcov_R[k, :P, :P]
         assert np.all(np.tril(R, -1) == 0)
         want = (2.4 ** 2 / P) * C
-        np.testing.assert_allclose(R.T @ R, want, rtol=1e-6, atol=1e-6 * np.abs(want).max())
+        np.testing.assert_allclose(R.T @ R, want, rtol=1e-10, atol=1e-10 * np.abs(want).max())  # FP64 R, P <= 520

@@ -550,9 +550,10 @@ struct DevAllocs {
   }
 };
 
-// One DRAM step: propose -> ssfun -> accept/propose stage 2 -> ssfun -> accept, sigma2, record
-// -> [adapt] -> step + 1.
-int enqueue_step(tci_ctx* ctx, const tci::DramState& st, const tci::DramParams& p, hipStream_t s, bool with_adapt) {
+// One DRAM step: propose -> ssfun -> accept/propose stage 2 -> ssfun -> accept, sigma2, log the row
+// -> [window records] -> [adapt] -> step + 1.
+int enqueue_step(tci_ctx* ctx, const tci::DramState& st, const tci::DramParams& p, hipStream_t s, bool with_stats,
+                 bool with_adapt) {
   int rc;
   if ((rc = tci::dram_launch_propose1(st, p, s)) != TCI_OK) return rc;
   if ((rc = tci::launch(ctx->kp, ctx->rpl, tci::MODE_SS, st.prop1, st.ld, st.cell, st.act1, st.n_chains, st.ss1,
@@ -563,6 +564,7 @@ int enqueue_step(tci_ctx* ctx, const tci::DramState& st, const tci::DramParams& 
                                        st.n_chains, st.ss2, nullptr, 0, s)) != TCI_OK)
     return rc;
   if ((rc = tci::dram_launch_accept2(st, p, s)) != TCI_OK) return rc;
+  if (with_stats && (rc = tci::dram_launch_stats(st, p, s)) != TCI_OK) return rc;
   if (with_adapt && (rc = tci::dram_launch_adapt(st, p, s)) != TCI_OK) return rc;  // no-op unless step % adaptint == 0
   return tci::dram_launch_step_incr(st, s);
 }
@@ -625,7 +627,14 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   hipError_t e = hipSuccess;
   tci::DramState st{};
   tci::DramParams p{};
-  const int64_t win = std::max<int64_t>(opt->adaptint, 1);
+  // Chunk of chain rows per fused-engine pass (its draws buffer holds one chunk; at most the next
+  // adaptation row) and the window slots per chain: the covupd window (adaptint rows), which is also
+  // the fused engines' per-row log of a chunk; without adaptation the log holds one chunk.
+  const int64_t ai = opt->adaptint;
+  const int64_t DW = tci::draw_stride(ld);
+  const int64_t chunk_cap = std::max<int64_t>(32, (int64_t)(((size_t)2 << 30) / (n * (size_t)DW * sizeof(double))));
+  const int64_t chunk = std::min<int64_t>(ai > 0 ? ai : 1000, chunk_cap);
+  const int64_t win = ai > 0 ? ai : chunk;
   const int64_t n_keep = opt->thin > 0 ? (opt->n_steps + opt->thin - 1) / opt->thin : 0;
   st.n_chains = n_chains;
   st.ld = ld;
@@ -659,13 +668,17 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(ss, double, n);
   TCI_ALLOC(prior, double, n);
   TCI_ALLOC(sigma2, double, n);
-  TCI_ALLOC(Rf, float, n * tci::dram_tri_stride(L));
+  TCI_ALLOC(Rd, double, n * tci::dram_tri_stride(L));
   TCI_ALLOC(cov, double, n * L2);
   TCI_ALLOC(work, double, p_max_all > 208 ? n * (size_t)((L + 15) / 16 * 16) * ((L + 15) / 16 * 16) : 1);
   TCI_ALLOC(cmean, double, n * L);
   TCI_ALLOC(wsum, double, n);
   TCI_ALLOC(window, double, n * (size_t)win * L);
   TCI_ALLOC(wsumv, double, n * L);
+  TCI_ALLOC(wacc1, double, n * L);
+  TCI_ALLOC(wacc2, double, n * L);
+  TCI_ALLOC(s2acc, double, n * 3);
+  TCI_ALLOC(s2log, double, n * (size_t)win);
   TCI_ALLOC(prop1, double, n * L);
   TCI_ALLOC(prop2, double, n * L);
   TCI_ALLOC(act1, uint8_t, n);
@@ -723,12 +736,18 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   p.stats_from = std::max<int64_t>(opt->stats_from, 1);
   p.thin = opt->thin;
   p.n_keep = n_keep;
+  p.win = win;
   // initial state: R = chol(J0), prior, sigma2, the initial ssfun call, chain row 1
   if ((rc = tci::dram_launch_init(st, d_qdiag, d_s20, s)) != TCI_OK) return fail(ctx, rc, "dram init launch");
   if ((rc = tci::launch(ctx->kp, ctx->rpl, tci::MODE_SS, st.theta, ld, d_cell, nullptr, n_chains, st.ss, nullptr, 0,
                         s)) != TCI_OK)
     return fail(ctx, rc, "initial ssfun launch");
   if ((rc = tci::dram_launch_init_stats(st, p, s)) != TCI_OK) return fail(ctx, rc, "dram stats launch");
+  if (win == 1) {  // one-row windows: row 1 is a window of its own
+    const int64_t one = 1;
+    TCI_HIP(ctx, hipMemcpyAsync(st.step, &one, sizeof(int64_t), hipMemcpyHostToDevice, s));
+    if ((rc = tci::dram_launch_stats(st, p, s)) != TCI_OK) return fail(ctx, rc, "dram stats launch");
+  }
   const int64_t two = 2;
   TCI_HIP(ctx, hipMemcpyAsync(st.step, &two, sizeof(int64_t), hipMemcpyHostToDevice, s));
   hipEvent_t ev0, ev1;
@@ -738,7 +757,6 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   int64_t p_max = 0;
   for (size_t c = 0; c < n; ++c) p_max = std::max<int64_t>(p_max, npar[c]);
   p.pmax = p_max;
-  const int64_t ai = opt->adaptint;
   // the fused engine's draws pass keeps a chain's R (packed fp32) and a tile of normals and products
   // in LDS: it must fit a CU (160 KB). AUTO picks it whenever it fits: measured on config 4 (10,000
   // chains x 200 points, 39 per CU) its chain walk + draws pass take 209 us per step against 1950 us
@@ -760,17 +778,17 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   if (fused && !fused_fits) return fail(ctx, TCI_ERANGE, "tci_dram_run: rows too long for the fused engine");
   if (fused) {
     // Chunks of chain rows up to the next adaptation row (and at most p.chunk rows: the draws
-    // buffer holds one chunk); k_chain leaves *st.step at the chunk end.
-    const int64_t DW = tci::draw_stride(ld);
-    const int64_t want = ai > 0 ? ai : 1000;
-    const int64_t cap = std::max<int64_t>(32, (int64_t)(((size_t)2 << 30) / (n * (size_t)DW * sizeof(double))));
-    p.chunk = std::min(want, cap);
+    // buffer holds one chunk); k_chain leaves *st.step at the chunk end. Per chunk: the draws pass
+    // and the walk (dram_launch_chain, which also keeps a completed window's records), and at an
+    // adaptation row the adaptation.
+    p.chunk = chunk;
     st.draws = A.alloc<double>(n * (size_t)p.chunk * DW, &e);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dram draws)");
     for (int64_t next = 2; next <= opt->n_steps && rc == TCI_OK;) {
       int64_t end = std::min<int64_t>(opt->n_steps, next + p.chunk - 1);
-      if (ai > 0) end = std::min<int64_t>(end, ((next + ai - 1) / ai) * ai);
-      rc = tci::dram_launch_chain(st, p, ctx->kp, ctx->rpl, next, end, s);
+      end = std::min<int64_t>(end, ((next + win - 1) / win) * win);  // chunks never cross a window
+      const int rec = end % win == 0 || end == opt->n_steps;  // the records kept in the chain kernel
+      rc = tci::dram_launch_chain(st, p, ctx->kp, ctx->rpl, next, end, rec, s);
       if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(st, p, s);
       next = end + 1;
     }
@@ -781,15 +799,16 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   // as a hipGraph and replayed; the head (steps 2..adaptint) and the tail run as plain launches.
   int64_t next = 2;  // next step number to enqueue
   auto plain = [&](int64_t upto) {  // steps next .. upto
-    for (; next <= upto && rc == TCI_OK; ++next) rc = enqueue_step(ctx, st, p, s, ai > 0 && next % ai == 0);
+    for (; next <= upto && rc == TCI_OK; ++next)
+      rc = enqueue_step(ctx, st, p, s, next % win == 0, ai > 0 && next % ai == 0);
   };
-  const int64_t G = ai > 0 ? ai : 50;
-  if (ai > 0) plain(std::min<int64_t>(ai, opt->n_steps));  // head: up to the first adaptation step
+  const int64_t G = win;  // graph blocks of one window (win = adaptint when adapting)
+  plain(std::min<int64_t>(win, opt->n_steps));  // head: up to the first window's end
   const int64_t blocks = (opt->n_steps - next + 1) / G;
   if (rc == TCI_OK && blocks > 0) {
     TCI_HIP(ctx, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     int crc = TCI_OK;
-    for (int64_t k = 0; k < G && crc == TCI_OK; ++k) crc = enqueue_step(ctx, st, p, s, ai > 0 && k == G - 1);
+    for (int64_t k = 0; k < G && crc == TCI_OK; ++k) crc = enqueue_step(ctx, st, p, s, k == G - 1, ai > 0 && k == G - 1);
     hipError_t ce = hipStreamEndCapture(s, &graph);
     if (crc != TCI_OK || ce != hipSuccess) {
       if (graph) (void)hipGraphDestroy(graph);
@@ -805,6 +824,12 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   }
   if (e == hipSuccess) plain(opt->n_steps);  // tail
   }
+  // the last, partial window's records (the fused engines: kept by the last chunk's kernel)
+  if (e == hipSuccess && rc == TCI_OK && opt->n_steps % win != 0 && !(fused && opt->n_steps >= 2)) {
+    const int64_t last = opt->n_steps;
+    rc = hipMemcpyAsync(st.step, &last, sizeof(int64_t), hipMemcpyHostToDevice, s) == hipSuccess ? TCI_OK : TCI_EHIP;
+    if (rc == TCI_OK) rc = tci::dram_launch_stats(st, p, s);
+  }
   const hipError_t ge = e;
   TCI_HIP(ctx, hipEventRecord(ev1, s));
   TCI_HIP(ctx, hipStreamSynchronize(s));
@@ -814,9 +839,17 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   {
     int64_t ph[8];
     TCI_HIP(ctx, hipMemcpy(ph, st.prof, sizeof(ph), hipMemcpyDeviceToHost));
-    std::fprintf(stderr, "{\"k_chain_cycles_per_chain\": [");
+    // TCI_CHAIN_PROFILE=1: slots 0-6 are wave 0's cycles per phase; slot 5 also counts the rounds
+    // in its bits 40+ (decoded here). =2: per-wave barrier waits (0-3) and pre-barrier work (4-7).
+    // TCI_ADAPT_PROFILE: thread 0's cycles per adaptation phase. All summed over the chains.
+    double rounds = 0.0;
+#if defined(TCI_CHAIN_PROFILE) && TCI_CHAIN_PROFILE == 1
+    rounds = (double)((uint64_t)ph[5] >> 40) / (double)n;
+    ph[5] = (int64_t)((uint64_t)ph[5] & ((1ull << 40) - 1));
+#endif
+    std::fprintf(stderr, "{\"cycles_per_chain\": [");
     for (int k = 0; k < 8; ++k) std::fprintf(stderr, "%s%.1f", k ? ", " : "", (double)ph[k] / (double)n);
-    std::fprintf(stderr, "]}\n");
+    std::fprintf(stderr, "], \"rounds_per_chain\": %.1f}\n", rounds);
   }
 #endif
   if (ge != hipSuccess) return hip_fail(ctx, ge, "DRAM step replay");
@@ -852,17 +885,17 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   if (out->final_theta) TCI_HIP(ctx, hipMemcpy(out->final_theta, st.theta, n * L * sizeof(double), hipMemcpyDeviceToHost));
   if (st.chain_out && out->chain)
     TCI_HIP(ctx, hipMemcpy(out->chain, st.chain_out, (size_t)n_keep * n * L * sizeof(double), hipMemcpyDeviceToHost));
-  if (out->qcov_R) {  // the device keeps R as packed fp32 upper triangles (exact: R is float-representable)
+  if (out->qcov_R) {  // the device keeps R as packed FP64 upper triangles
     const int64_t ts = tci::dram_tri_stride((int64_t)L);
-    std::vector<float> rf((size_t)n * ts);
-    TCI_HIP(ctx, hipMemcpy(rf.data(), st.Rf, rf.size() * sizeof(float), hipMemcpyDeviceToHost));
+    std::vector<double> rd((size_t)n * ts);
+    TCI_HIP(ctx, hipMemcpy(rd.data(), st.Rd, rd.size() * sizeof(double), hipMemcpyDeviceToHost));
     for (size_t c = 0; c < n; ++c) {
       double* R = out->qcov_R + c * L2;
       std::fill(R, R + L2, 0.0);
       const int64_t P = npar[c];
-      const float* src = rf.data() + c * ts;
+      const double* src = rd.data() + c * ts;
       for (int64_t i = 0, e = 0; i < P; ++i)
-        for (int64_t j = i; j < P; ++j, ++e) R[i * L + j] = (double)src[e];
+        for (int64_t j = i; j < P; ++j, ++e) R[i * L + j] = src[e];
     }
   }
   if (st.s2_out && out->s2chain)

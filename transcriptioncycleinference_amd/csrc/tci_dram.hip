@@ -20,11 +20,10 @@
 //             burnin_scale when the window's rejection rate is > 0.95 or < 0.05; afterwards
 //             covupd over all chain rows so far, R = chol(cov + qcovadj*I) * adascale
 //   prior     sum(((theta - mu)./sig).^2) over parameters with finite sig (dR: N(0, 50), :254)
-// The proposal factor R is kept with float-representable entries (rounded once when it is set),
-// so a chain's R is held exactly as a packed fp32 upper triangle (P(P+1)/2 floats: DramState::Rf,
-// the only device copy) and fits in LDS for the proposal products; the proposal covariance is then
-// R'R of that rounded R, consistently in both stages (a 1e-7-relative change of the proposal
-// shape; the sampler stays exact for it).
+// The proposal factor R is FP64, as mcmcstat's double chol: a chain's R is a packed upper triangle
+// (P(P+1)/2 doubles: DramState::Rd, the only device copy), staged into LDS for the proposal
+// products while it fits beside a pass of normals (every TestData cell), read from global memory
+// beyond (configs 4/5) in the same MFMA order.
 // Randomness: Philox4x32-10 keyed by (seed), counter (chain, step, purpose, index) -- the
 // stream is reproducible and independent of launch geometry (MATLAB's MT19937 is not
 // reproducible here, so chain parity with the reference is statistical only).
@@ -212,45 +211,42 @@ __device__ double prior_ss(const double* th, const double* mu, const double* sig
   return block_sum(s, red);
 }
 
-// Proposal factor entries are kept float-representable (see the header).
-__device__ __forceinline__ double f32_round(double x) { return (double)(float)x; }
-
-// Packed upper triangle (row i at i*P - i*(i-1)/2) of a chain's R as fp32: st.Rf holds it in
-// global memory (chain c at c * tri_stride(ld)), written beside every write of R (store_R), so a
-// workgroup stages it into LDS with one coalesced copy.
+// Packed upper triangle (row i at i*P - i*(i-1)/2) of a chain's R in FP64 -- mcmcstat's double
+// chol -- (st.Rd, chain c at c * tri_stride(ld), the only device copy), so a workgroup stages it
+// into LDS with one coalesced copy.
 __device__ __forceinline__ int tri_off(int i, int P) { return i * P - (i * (i - 1)) / 2; }
 __host__ __device__ inline int64_t tri_stride(int64_t ld) { return dram_tri_stride(ld); }
 __device__ __forceinline__ void store_R(const DramState& st, int64_t c, int P, int i, int j, double v) {
-  if (j >= i) st.Rf[c * tri_stride(st.ld) + tri_off(i, P) + j - i] = (float)v;
+  if (j >= i) st.Rd[c * tri_stride(st.ld) + tri_off(i, P) + j - i] = v;
 }
-// Burn-in scaling R <- f32_round(R * s), on the packed triangle (the lower triangle is zero).
+// Burn-in scaling R <- R * s, on the packed triangle (the lower triangle is zero).
 __device__ __forceinline__ void scale_R(const DramState& st, int64_t c, int P, double s, int t, int nth) {
-  float* Rf = st.Rf + c * tri_stride(st.ld);
-  for (int e = t; e < P * (P + 1) / 2; e += nth) Rf[e] = (float)((double)Rf[e] * s);
+  double* Rd = st.Rd + c * tri_stride(st.ld);
+  for (int e = t; e < P * (P + 1) / 2; e += nth) Rd[e] = Rd[e] * s;
 }
-// The same copy by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction, no registers):
-// every piece is in flight at once, and the caller's next work (the draws pass's normals) runs
-// while they land; the caller's __syncthreads waits for them. Rl: 16-byte aligned, room for the
-// triangle rounded up to 256 floats (the source stride is, dram_tri_stride).
+// The copy by LDS-DMA (global_load_lds_dwordx4: 1 KiB = 128 doubles per wave-instruction, no
+// registers): every piece is in flight at once, and the caller's next work (the draws pass's
+// normals) runs while they land; the caller waits for vmcnt and then barriers. Rl: 16-byte aligned,
+// room for the triangle rounded up to 128 doubles (the source stride is, dram_tri_stride).
 template <int NTH>
-__device__ __forceinline__ void load_R_glds(float* Rl, const DramState& st, int64_t c, int P) {
-  const float* src = st.Rf + c * tri_stride(st.ld);
-  const int pieces = (P * (P + 1) / 2 + 255) >> 8;
+__device__ __forceinline__ void load_R_glds(double* Rl, const DramState& st, int64_t c, int P) {
+  const double* src = st.Rd + c * tri_stride(st.ld);
+  const int pieces = (P * (P + 1) / 2 + 127) >> 7;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   for (int k = w; k < pieces; k += NTH / 64)
-    __builtin_amdgcn_global_load_lds((const void*)(src + 256 * k + 4 * lane),
-                                     (__attribute__((address_space(3))) void*)(Rl + 256 * k), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(src + 128 * k + 2 * lane),
+                                     (__attribute__((address_space(3))) void*)(Rl + 128 * k), 16, 0, 0);
 }
 template <int NTH = kThreads>
-__device__ void load_R_f32(float* Rl, const DramState& st, int64_t c, int P) {
-  const float* src = st.Rf + c * tri_stride(st.ld);
+__device__ void load_R(double* Rl, const DramState& st, int64_t c, int P) {
+  const double* src = st.Rd + c * tri_stride(st.ld);
   const int tri = P * (P + 1) / 2;
 #pragma unroll 4
   for (int e = threadIdx.x; e < tri; e += NTH) Rl[e] = src[e];
 }
 
 // Proposal products U[r][j] = sum_{i<=j} Z[r][i] R[i][j] for r < M <= 16*MT rows of normals (LDS,
-// row stride zs) and the chain's packed fp32 R (LDS); store(r, j, value) receives every product.
+// row stride zs) and the chain's packed FP64 R (LDS or global); store(r, j, value) receives every product.
 // One v_mfma_f64_16x16x4_f64 per 4-row k-step of a 16 x 16 (row tile, column tile) block:
 // A = Z[row = lane&15][k = lane>>4], B = R[k = lane>>4][col = lane&15], D row = (lane>>4) + 4 q,
 // col = lane&15 (cdna_hip_programming.md f64 MFMA map). Column tiles go to the 4 waves in snake order
@@ -266,7 +262,7 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // PF > 0 (R in global memory): every k-step also loads the R values of all CT tiles PF k-steps
 // ahead, so an L2/HBM round trip overlaps PF k-steps' MFMAs instead of preceding them.
 template <int MT, int CT, int NWV, class Store, int PF = 0>  // NWV: waves sharing the column tiles; PF: prefetch depth
-__device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const float* Rl, int P, int top, Store store) {
+__device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const double* Rl, int P, int top, Store store) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int row = lane & 15, kq = lane >> 4;
   int nt[CT], kmx[CT];
@@ -285,7 +281,7 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
     for (int m = 0; m < MT; ++m) acc[g][m] = f64x4{0.0, 0.0, 0.0, 0.0};
   int i0 = 0;
   // raw R values of k-step i0n for every tile (inactive tiles read a valid clamped entry)
-  auto load_b = [&](int i0n, float* b) {
+  auto load_b = [&](int i0n, double* b) {
     const int icn = min(i0n + kq, P - 1);
     const int tof = tri_off(icn, P) - icn;
 #pragma unroll
@@ -294,7 +290,7 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
       b[g] = Rl[tof + (jc >= icn ? jc : icn)];
     }
   };
-  float bq[PF > 0 ? PF : 1][CT];  // bq[d]: k-step i0 + 4 d (rotated every step)
+  double bq[PF > 0 ? PF : 1][CT];  // bq[d]: k-step i0 + 4 d (rotated every step)
 #pragma unroll
   for (int d = 0; d < PF; ++d) load_b(4 * d, bq[d]);
 #pragma unroll
@@ -302,7 +298,7 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
     for (; i0 <= kmx[ng - 1]; i0 += 4) {  // tiles g < ng still need k-step i0
       const int i = i0 + kq;
       const int ic = i < P ? i : P - 1;
-      float bcur[CT];
+      double bcur[CT];
       if (PF > 0) {
 #pragma unroll
         for (int g = 0; g < CT; ++g) bcur[g] = bq[0][g];
@@ -324,8 +320,8 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
       for (int g = 0; g < ng; ++g) {
         const int j = 16 * nt[g] + row;
         const int jc = j < P ? j : P - 1;
-        const float rv = PF > 0 ? bcur[g] : Rl[toff + (jc >= ic ? jc : ic)];
-        const double b = (i <= j && j < P) ? (double)rv : 0.0;
+        const double rv = PF > 0 ? bcur[g] : Rl[toff + (jc >= ic ? jc : ic)];
+        const double b = (i <= j && j < P) ? rv : 0.0;
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[g][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b, acc[g][m], 0, 0, 0);
       }
@@ -347,26 +343,26 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const fl
 constexpr int kZrCT = 5;  // column tiles per wave and call: 20 per 4-wave call (P <= 320 in one call)
 
 // Dynamic LDS of the per-stage kernels (vector stride L = ld >= P): z, y, red and the chain's R
-// as packed fp32.
+// as packed FP64.
 struct Smem {
   double* z;
   double* y;
   double* red;
-  float* Rl;
+  double* Rl;
   int L;
 };
-// R is staged into LDS only while it fits (stage_r_lds); longer rows read the packed fp32 R from
+// R is staged into LDS only while it fits (stage_r_lds); longer rows read the packed R from
 // global memory in the same MFMA order (the same bits).
-__host__ __device__ inline bool stage_r_lds(int64_t L) { return (2 * L + 8) * 8 + (L * (L + 1) / 2) * 4 + 16 <= 150 * 1024; }
+__host__ __device__ inline bool stage_r_lds(int64_t L) { return (2 * L + 8) * 8 + (L * (L + 1) / 2) * 8 + 16 <= 150 * 1024; }
 __host__ __device__ inline int64_t stage_lds_bytes(int64_t L) {
-  return (2 * L + 8) * 8 + (stage_r_lds(L) ? (L * (L + 1) / 2) * 4 : 0) + 16;
+  return (2 * L + 8) * 8 + (stage_r_lds(L) ? (L * (L + 1) / 2) * 8 : 0) + 16;
 }
 __device__ __forceinline__ Smem stage_smem(double* dyn, int L) {
   Smem m;
   m.z = dyn;
   m.y = dyn + L;
   m.red = dyn + 2 * L;
-  m.Rl = reinterpret_cast<float*>(dyn + 2 * L + 8);
+  m.Rl = dyn + 2 * L + 8;
   m.L = L;
   return m;
 }
@@ -402,14 +398,14 @@ __device__ bool propose_block(const DramState& st, const DramParams& p, int64_t 
   const int64_t ld = st.ld;
   draw_normals(p.seed, st.key[c], step, purpose, P, sm.z, threadIdx.x);
   const bool rl = stage_r_lds(st.ld);
-  if (rl) load_R_f32(sm.Rl, st, c, P);
+  if (rl) load_R(sm.Rl, st, c, P);
   __syncthreads();
   double* U = sm.y;
   const int us = sm.L;
   const auto put = [=](int r, int j, double v) { U[r * us + j] = v; };
   for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= 4 * kZrCT) {
     if (rl) mfma_zr<1, kZrCT, 4>(sm.z, sm.L, 1, sm.Rl, P, top, put);  // two calls: each one's R pointer has
-    else mfma_zr<1, kZrCT, 4>(sm.z, sm.L, 1, st.Rf + c * tri_stride(st.ld), P, top, put);  // a known address space
+    else mfma_zr<1, kZrCT, 4>(sm.z, sm.L, 1, st.Rd + c * tri_stride(st.ld), P, top, put);  // a known address space
   }
   __syncthreads();
   int inb = 1;
@@ -431,10 +427,10 @@ __global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* _
   const int P = st.npar[c];
   double* cv = st.cov + c * ld * ld;
   for (int64_t e = threadIdx.x; e < ld * ld; e += kThreads) cv[e] = 0.0;
-  for (int64_t e = threadIdx.x; e < tri_stride(ld); e += kThreads) st.Rf[c * tri_stride(ld) + e] = 0.0f;
+  for (int64_t e = threadIdx.x; e < tri_stride(ld); e += kThreads) st.Rd[c * tri_stride(ld) + e] = 0.0;
   __syncthreads();
   for (int j = threadIdx.x; j < P; j += kThreads) {
-    store_R(st, c, P, j, j, f32_round(sqrt(qdiag[c * ld + j])));  // R = chol(qcov), qcov = J0 diagonal (:230)
+    store_R(st, c, P, j, j, sqrt(qdiag[c * ld + j]));  // R = chol(qcov), qcov = J0 diagonal (:230)
     st.cmean[c * ld + j] = 0.0;
   }
   const double pr = prior_ss(st.theta + c * ld, st.pmu + c * ld, st.psig + c * ld, P, red);
@@ -448,67 +444,36 @@ __global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* _
   }
 }
 
-// Chain row `row` (1-based) = the current state th (global or LDS): the covupd window row, the
-// posterior Welford stats (mean/M2 arrays in global or LDS) and the thinned output row; entries
-// j = j0, j0 + js, .. of the row.
-__device__ void record_vec(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P, const double* th,
-                           double* smean, double* sm2, int j0, int js) {
-  const int64_t ld = st.ld;
-  if (p.adaptint > 0) {
-    const int64_t slot = (row - 1) % p.adaptint;
-    double* w = st.window + (c * p.adaptint + slot) * ld;
-    double* ws = st.wsumv + c * ld;  // the window's column sums, in row order (adaptation's batch mean)
-    for (int j = j0; j < P; j += js) {
-      w[j] = th[j];
-      ws[j] = slot == 0 ? th[j] : ws[j] + th[j];
-    }
-  }
-  if (row >= p.stats_from) {  // posterior mean / population std over chain(stats_from:end, :) (:276-301)
-    const double n = (double)(row - p.stats_from + 1);
-    for (int j = j0; j < P; j += js) {
-      const double x = th[j];
-      double m = smean[j];
-      const double d = x - m;
-      m += d / n;
-      smean[j] = m;
-      sm2[j] += d * (x - m);
-    }
-  }
-  if (st.chain_out != nullptr && p.thin > 0 && (row - 1) % p.thin == 0) {
-    const int64_t k = (row - 1) / p.thin;
-    if (k < p.n_keep)
-      for (int j = j0; j < P; j += js) st.chain_out[(k * st.n_chains + c) * ld + j] = th[j];
-  }
+// ---- Chain records. Every engine LOGS each chain row: the state into its window slot
+// (DramState::window, slot (row - 1) % p.win, the covupd window when adapting) and its s2 into the
+// same slot of DramState::s2log. The records are kept window by window (p.win rows from row 1, the
+// same partition for every engine):
+//   * the window's column sums (the adaptation's batch mean);
+//   * the posterior mean / M2 of rows >= stats_from (:276-301): the window's rows as one batch --
+//     shifted sums S1 = sum(x - K), S2 = sum((x - K)^2) with K the running mean (or, before any
+//     statistics row, the window's first row), batch mean K + S1/nb and M2 S2 - S1^2/nb -- merged
+//     into the running values by the pairwise formula (Chan, Golub & LeVeque): the Welford
+//     recurrence's result in exact arithmetic, with no per-row division;
+//   * the same for sqrt(s2) over all rows and the sum of s2 (:302-303);
+//   * the thinned output rows.
+// Every sum runs over the window's rows in row order from 0.0, so every engine has the same bits:
+// k_chain adds each row as it is decided (ColAcc / S2Acc on its record waves; a window that spans
+// chunks continues from DramState::wsumv / wacc1 / wacc2 / s2acc), k_walk and k_stats read the
+// window's logs back at its end (window_records).
+__device__ __forceinline__ int64_t log_slot(const DramParams& p, int64_t row) { return (row - 1) % p.win; }
+
+// The batched engine's per-step log (one workgroup per chain).
+__device__ void log_row_block(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P, const double* th,
+                              double s2) {
+  const int64_t slot = log_slot(p, row);
+  double* w = st.window + (c * p.win + slot) * st.ld;
+  for (int j = threadIdx.x; j < P; j += kThreads) w[j] = th[j];
+  if (threadIdx.x == 0) st.s2log[c * p.win + slot] = s2;
 }
 
-// The s2 statistics of chain row `row` over the whole s2chain (:302-303) and its thinned s2.
 struct S2Stats {
   double sum, qmean, qm2;
 };
-__device__ void record_s2(const DramState& st, const DramParams& p, int64_t c, int64_t row, double s2, S2Stats& a) {
-  a.sum += s2;
-  const double q = sqrt(s2), n = (double)row;
-  const double d = q - a.qmean;
-  a.qmean += d / n;
-  a.qm2 += d * (q - a.qmean);
-  if (st.s2_out != nullptr && p.thin > 0 && (row - 1) % p.thin == 0) {
-    const int64_t k = (row - 1) / p.thin;
-    if (k < p.n_keep) st.s2_out[k * st.n_chains + c] = s2;
-  }
-}
-
-// Both parts for the per-stage kernels (global stats).
-__device__ void record_row(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P, const double* th,
-                           double s2) {
-  record_vec(st, p, c, row, P, th, st.smean + c * st.ld, st.sm2 + c * st.ld, threadIdx.x, kThreads);
-  if (threadIdx.x == 0) {
-    S2Stats a{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
-    record_s2(st, p, c, row, s2, a);
-    st.s2sum[c] = a.sum;
-    st.sq_mean[c] = a.qmean;
-    st.sq_m2[c] = a.qm2;
-  }
-}
 
 __global__ __launch_bounds__(kThreads) void k_init_stats(DramState st, DramParams p) {
   const int64_t c = blockIdx.x;
@@ -523,8 +488,24 @@ __global__ __launch_bounds__(kThreads) void k_init_stats(DramState st, DramParam
     st.sq_mean[c] = 0.0;
     st.sq_m2[c] = 0.0;
   }
-  __syncthreads();
-  record_row(st, p, c, 1, P, st.theta + c * st.ld, st.sigma2[c]);
+  log_row_block(st, p, c, 1, P, st.theta + c * st.ld, st.sigma2[c]);  // chain row 1: the initial state
+  // k_chain's running sums of the first window after row 1 (ColAcc / S2Acc::add of row 1, K = row 1)
+  const bool in_stats = p.stats_from <= 1;
+  for (int j = threadIdx.x; j < P; j += kThreads) {
+    const double x = st.theta[c * st.ld + j], d = x - x;
+    st.wsumv[c * st.ld + j] = 0.0 + x;
+    st.wacc1[c * st.ld + j] = in_stats ? 0.0 + d : 0.0;
+    st.wacc2[c * st.ld + j] = in_stats ? fma(d, d, 0.0) : 0.0;
+  }
+  if (st.chain_out != nullptr && p.thin > 0 && p.n_keep > 0)  // row 1 is always kept (k_chain writes rows >= 2)
+    for (int j = threadIdx.x; j < P; j += kThreads) st.chain_out[c * st.ld + j] = st.theta[c * st.ld + j];
+  if (threadIdx.x == 0) {
+    if (st.s2_out != nullptr && p.thin > 0 && p.n_keep > 0) st.s2_out[c] = st.sigma2[c];
+    const double s2 = st.sigma2[c], dq = sqrt(s2) - sqrt(s2);
+    st.s2acc[3 * c + 0] = 0.0 + s2;
+    st.s2acc[3 * c + 1] = 0.0 + dq;
+    st.s2acc[3 * c + 2] = fma(dq, dq, 0.0);
+  }
 }
 
 __global__ __launch_bounds__(kThreads) void k_propose1(DramState st, DramParams p) {
@@ -619,7 +600,7 @@ __global__ __launch_bounds__(kThreads) void k_accept2(DramState st, DramParams p
     if (p.updatesigma) st.sigma2[c] = 1.0 / gamma_at(p.seed, st.key[c], step, 0.5 * (double)st.nobs[c], 2.0 / st.ss[c]);
   }
   __syncthreads();
-  record_row(st, p, c, step, P, st.theta + c * st.ld, st.sigma2[c]);
+  log_row_block(st, p, c, step, P, st.theta + c * st.ld, st.sigma2[c]);
 }
 
 __global__ void k_step_incr(int64_t* step) {
@@ -678,14 +659,14 @@ constexpr int kDrawPassesGR = 4;
 enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
 
 // Dynamic LDS of k_draws: one pass's normals (2 x kDrawSteps rows of stride L) and the chain's R
-// as packed fp32.
-// R is staged only while it fits beside the normals; longer rows read the packed fp32 R from global
+// as packed FP64 (P <= 150 or so: every TestData cell).
+// R is staged only while it fits beside the normals; longer rows read the packed R from global
 // memory in the same MFMA order (the same bits).
 __host__ __device__ inline bool draws_r_lds(int64_t L) {
-  return (2 * kDrawSteps * L) * 8 + dram_tri_stride(L) * 4 + 16 <= 160 * 1024;
+  return (2 * kDrawSteps * L) * 8 + dram_tri_stride(L) * 8 + 16 <= 160 * 1024;
 }
 __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
-  return (2 * kDrawSteps * L) * 8 + (draws_r_lds(L) ? dram_tri_stride(L) * 4 : 0) + 16;
+  return (2 * kDrawSteps * L) * 8 + (draws_r_lds(L) ? dram_tri_stride(L) * 8 : 0) + 16;
 }
 // WALK (thousands of chains, one draws workgroup per CU): passes per workgroup with R in LDS,
 // so R is staged once per 64 steps (configs 4/5: 174.3 -> 171.6 us per step; 7 passes: 171.9)
@@ -714,10 +695,10 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
   const int64_t DW = draw_stride(ld);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   double* Z = dyn;
-  float* Rl = reinterpret_cast<float*>(Z + 2 * kDrawSteps * L);
+  double* Rl = Z + 2 * kDrawSteps * L;
   const bool rl = draws_r_lds(ld);
   if (rl && !(TCI_DRAWS_ABLATE & 8)) load_R_glds<kDrawThreads>(Rl, st, c, P);
-  const float* Rg = st.Rf + c * tri_stride(ld);
+  const double* Rg = st.Rd + c * tri_stride(ld);
   const double a = 0.5 * (double)st.nobs[c];
   const double inv_ds = 1.0 / p.drscale;
   double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
@@ -774,69 +755,164 @@ __device__ __forceinline__ double wave_prior_reg(const double* y, const double* 
   return wsum64(s);
 }
 
-// Where chain row `row` goes, advanced row by row without 64-bit divisions on the step path:
-// its covupd window slot (row - 1) % adaptint and, when (row - 1) % thin == 0, its output row.
-struct RowCursor {
-  int64_t win, tpos, keep;  // window slot; (row - 1) % thin; (row - 1) / thin
-  __device__ void init(const DramParams& p, int64_t row) {
-    win = p.adaptint > 0 ? (row - 1) % p.adaptint : 0;
-    tpos = p.thin > 0 ? (row - 1) % p.thin : 1;
-    keep = p.thin > 0 ? (row - 1) / p.thin : 0;
-  }
-  __device__ void next(const DramParams& p) {
-    if (++win == p.adaptint) win = 0;
-    if (p.thin > 0 && ++tpos == p.thin) {
-      tpos = 0;
-      ++keep;
-    }
-  }
-  __device__ bool kept(const DramParams& p) const { return p.thin > 0 && tpos == 0 && keep < p.n_keep; }
-};
+// The fused engines' per-row logs (k_chain / k_walk: one wave writes a row).
+template <int NJ>
+__device__ __forceinline__ void log_row(const DramState& st, const DramParams& p, int64_t c, int64_t slot, int P,
+                                        const double* th, int lane) {
+  double* w = st.window + (c * p.win + slot) * st.ld;
+#pragma unroll
+  for (int k = 0; k < NJ; ++k)
+    if (lane + 64 * k < P) w[lane + 64 * k] = th[k];
+}
+__device__ __forceinline__ void log_s2(const DramState& st, const DramParams& p, int64_t c, int64_t slot, double s2) {
+  st.s2log[c * p.win + slot] = s2;
+}
 
-// record_vec on register-held vectors by one wave (smn/sm2: this lane's Welford entries): the same
-// stores and Welford arithmetic as record_vec.
-template <int NJ, int SS = 1>  // SS: stride of smn / sm2 / wsv entries (1: registers, 64: a wave's LDS rows)
-__device__ __forceinline__ void record_vec_reg(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P,
-                                               const double* th, double* smn, double* sm2, double* wsv,
-                                               int lane, const RowCursor& cur) {
-  const int64_t ld = st.ld;
-  if (p.adaptint > 0) {
-    double* w = st.window + (c * p.adaptint + cur.win) * ld;
-#pragma unroll
-    for (int k = 0; k < NJ; ++k) {
-      if (lane + 64 * k < P) w[lane + 64 * k] = th[k];
-      wsv[SS * k] = cur.win == 0 ? th[k] : wsv[SS * k] + th[k];  // as record_vec's column sums
-    }
+// Pairwise merge of a batch (nb values, shifted sums S1, S2 about K) into running (n, mean, M2).
+__device__ __forceinline__ void stats_merge(double na, double nb, double K, double S1, double S2, double& mean,
+                                            double& m2) {
+  if (nb <= 0.0) return;
+  const double db = S1 / nb;                 // batch mean - K
+  const double m2b = fma(-S1, db, S2);       // sum (x - mean_b)^2
+  if (na <= 0.0) {
+    mean = K + db;
+    m2 = m2b;
+    return;
   }
-  if (row >= p.stats_from) {
-    const double n = (double)(row - p.stats_from + 1);
+  const double n = na + nb, d = (K - mean) + db;  // batch mean - running mean
+  mean = fma(d, nb / n, mean);
+  m2 = m2 + m2b + d * d * (na * nb / n);
+}
+
+__device__ __forceinline__ int64_t win_first(const DramParams& p, int64_t row) { return (row - 1) / p.win * p.win + 1; }
+__device__ __forceinline__ bool kept_row(const DramParams& p, int64_t row, int64_t& k) {
+  if (p.thin <= 0 || (row - 1) % p.thin != 0) return false;
+  k = (row - 1) / p.thin;
+  return k < p.n_keep;
+}
+
+// A window's column sums (lanes: columns j = lane + 64 k, k < NJ), added row by row in row order.
+template <int NJ>
+struct ColAcc {
+  double ws[NJ], S1[NJ], S2[NJ], K[NJ];
+  int64_t first, sf;
+  bool kfirst;  // no statistics row before the window: K = the window's first row
+  __device__ void setup(const DramParams& p, int64_t row) {
+    first = win_first(p, row);
+    sf = max(first, p.stats_from);
+    kfirst = first <= p.stats_from;
+  }
+  __device__ void zero() {
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) ws[k] = S1[k] = S2[k] = K[k] = 0.0;
+  }
+  __device__ __forceinline__ void add(int64_t row, const double* x) {
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
-      if (lane + 64 * k < P) {
-        const double x = th[k];
-        double m = smn[SS * k];
-        const double d = x - m;
-        m += d / n;
-        smn[SS * k] = m;
-        sm2[SS * k] += d * (x - m);
+      if (kfirst && row == first) K[k] = x[k];
+      ws[k] = ws[k] + x[k];
+      if (row >= sf) {
+        const double d = x[k] - K[k];
+        S1[k] = S1[k] + d;
+        S2[k] = fma(d, d, S2[k]);
       }
     }
   }
-  if (st.chain_out != nullptr && cur.kept(p))
+  // the window's records at its last row `last` (columns jl + 64 k): merged into the running
+  // statistics, the column sums kept for the adaptation
+  __device__ void finish(const DramState& st, const DramParams& p, int64_t c, int64_t last, int P, int jl) {
+    const int64_t ld = st.ld;
+    const double na = (double)max<int64_t>(first - p.stats_from, 0), nb = (double)max<int64_t>(last - sf + 1, 0);
+    double mean[NJ], m2[NJ];
 #pragma unroll
-    for (int k = 0; k < NJ; ++k)
-      if (lane + 64 * k < P) st.chain_out[(cur.keep * st.n_chains + c) * ld + lane + 64 * k] = th[k];
+    for (int k = 0; k < NJ; ++k) {
+      const int j = jl + 64 * k;
+      mean[k] = j < P ? st.smean[c * ld + j] : 0.0;
+      m2[k] = j < P ? st.sm2[c * ld + j] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      const int j = jl + 64 * k;
+      stats_merge(na, nb, K[k], S1[k], S2[k], mean[k], m2[k]);
+      if (j < P) {
+        st.smean[c * ld + j] = mean[k];
+        st.sm2[c * ld + j] = m2[k];
+        st.wsumv[c * ld + j] = ws[k];
+      }
+    }
+  }
+};
+
+// The same for s2 (one value per row; lane 0 of k_chain's kSigWave, uniform in window_records).
+struct S2Acc {
+  double sum, S1, S2, K;
+  __device__ __forceinline__ void add(double s2) {
+    const double dq = sqrt(s2) - K;
+    sum = sum + s2;
+    S1 = S1 + dq;
+    S2 = fma(dq, dq, S2);
+  }
+  __device__ void finish(const DramState& st, int64_t c, int64_t first, int64_t last) {
+    double qmean = st.sq_mean[c], qm2 = st.sq_m2[c];
+    stats_merge((double)(first - 1), (double)(last - first + 1), K, S1, S2, qmean, qm2);
+    st.s2sum[c] += sum;
+    st.sq_mean[c] = qmean;
+    st.sq_m2[c] = qm2;
+  }
+};
+
+// The records of the window ending at row `last` from its logs, by one wave (k_walk at a window's
+// end, k_stats): the rows in row order, kStatsRows loads in flight per column block.
+constexpr int kStatsRows = 32;
+__device__ void window_records(const DramState& st, const DramParams& p, int64_t c, int64_t last, int lane) {
+  const int64_t ld = st.ld;
+  const int P = st.npar[c];
+  const int64_t first = win_first(p, last);
+  const int nrow = (int)(last - first + 1);
+  const double* win = st.window + c * p.win * ld;
+  ColAcc<1> a;
+  a.setup(p, first);
+  for (int j0 = 0; j0 < P; j0 += 64) {  // uniform
+    const int j = j0 + lane;
+    const int jj = j < P ? j : 0;
+    a.zero();
+    a.K[0] = a.kfirst ? 0.0 : (j < P ? st.smean[c * ld + j] : 0.0);
+    for (int rb = 0; rb < nrow; rb += kStatsRows) {
+      double x[kStatsRows];  // every load issued together (clamped rows: no branch between them)
+#pragma unroll
+      for (int u = 0; u < kStatsRows; ++u) x[u] = win[(int64_t)min(rb + u, nrow - 1) * ld + jj];
+#pragma unroll
+      for (int u = 0; u < kStatsRows; ++u) {
+        if (rb + u >= nrow) break;  // uniform
+        const int64_t row = first + rb + u;
+        a.add(row, &x[u]);
+        int64_t k;
+        if (st.chain_out != nullptr && j < P && kept_row(p, row, k)) st.chain_out[(k * st.n_chains + c) * ld + j] = x[u];
+      }
+    }
+    a.finish(st, p, c, last, P, j);
+  }
+  // s2: 64 rows per pass in lanes, added in row order through lane broadcasts
+  const double* lg = st.s2log + c * p.win;
+  S2Acc q{0.0, 0.0, 0.0, first > 1 ? st.sq_mean[c] : sqrt(lg[0])};
+  for (int r0 = 0; r0 < nrow; r0 += 64) {
+    const int r = r0 + lane;
+    const double v = lg[min(r, nrow - 1)];
+    int64_t k;
+    if (st.s2_out != nullptr && r < nrow && kept_row(p, first + r, k)) st.s2_out[k * st.n_chains + c] = v;
+    const int m = min(64, nrow - r0);
+    for (int l = 0; l < m; ++l) q.add(lane_bcast(v, l));
+  }
+  if (lane == 0) q.finish(st, c, first, last);
 }
 
-// record_s2 with the row's place from the cursor.
-__device__ __forceinline__ void record_s2_cur(const DramState& st, const DramParams& p, int64_t c, int64_t row,
-                                              double s2, S2Stats& a, const RowCursor& cur) {
-  a.sum += s2;
-  const double q = sqrt(s2), n = (double)row;
-  const double d = q - a.qmean;
-  a.qmean += d / n;
-  a.qm2 += d * (q - a.qmean);
-  if (st.s2_out != nullptr && cur.kept(p)) st.s2_out[cur.keep * st.n_chains + c] = s2;
+// The batched engine's records (and a run's first or last window outside a chunk): one wave per
+// chain, the window ending at row *st.step.
+__global__ __launch_bounds__(kThreads) void k_stats(DramState st, DramParams p) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * (kThreads / 64) + w;
+  if (c >= st.n_chains) return;
+  window_records(st, p, c, *st.step, lane);
 }
 
 #ifndef TCI_CHAIN_PROFILE
@@ -859,9 +935,8 @@ __device__ __forceinline__ uint64_t stamp() {
 
 // Which waves keep the chain records. Both are stage-1 waves: a stage-1 proposal is more often out
 // of bounds (it skips ssfun), so these waves reach the barrier first and have slack before it.
-//   kRecWave: window row + column sums + posterior Welford + thinned rows of the decided rows;
-//   kSigWave: the sigma2 chain (s2 of each decided row, its statistics and thinned rows) and the
-//             precisions 1/s2 the next decisions use.
+//   kRecWave: the window-slot log of the decided rows (log_row; k_stats keeps their records);
+//   kSigWave: the s2 of each decided row (log_s2) and the precisions 1/s2 the next decisions use.
 constexpr int kRecWave = 0, kSigWave = 2;  // (six placements measured within 1 %: r02u_record_wave_placement)
 // k_chain / k_walk loop heads: the lane index is re-laundered every round/step (launder_lane), so
 // the 64-bit lane masks derived from it are recomputed (one compare each) instead of living in
@@ -871,7 +946,7 @@ __device__ __forceinline__ void launder_lane(int& lane) { asm volatile("" : "+v"
 
 template <int RPL, int NSEG>
 __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
-                                                    int64_t s_end) {
+                                                    int64_t s_end, int with_records) {
   // Round structure (one workgroup barrier per round). At the start of a round the state after
   // row s-1 is known. Wave w evaluates proposal (stage w&1) of step s + (w>>1): waves 0/1 the
   // stage-1/2 proposals of step s, waves 2/3 those of step s+1 drawn around the SAME state, i.e.
@@ -887,7 +962,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   //   * the precisions the decisions use: 1/s2 of the current state (step s) and, for step s+1
   //     after an unmoved step s, 1/s2 with s2 = 1/(G_s*(2/ss)) -- both known before the round;
   //   * the s2 of the rows the previous round decided (1/(G*(2/ss)) of the state after them)
-  //     and the records of those rows.
+  //     and the logs of those rows (k_stats turns them into the records after the chunk).
   constexpr int NJ = RPL + 1;  // vector entries per lane: P = 7 + N <= 64 RPL + 8 <= 64 NJ
   constexpr int EV = eval_lds_doubles<RPL>();
   constexpr int NW = kThreads / 64;
@@ -898,14 +973,14 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int lane = threadIdx.x & 63;  // re-laundered every round (TCI_LOOP_LAUNDER)
+  int lane = threadIdx.x & 63;  // re-laundered every round (launder_lane)
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int64_t DW = draw_stride(ld);
   const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
   const int stage = w & 1, ahead = w >> 1;                        // this wave's proposal
   const double scale = stage ? 1.0 / p.drscale : 1.0;
-  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], smn[NJ], sm2[NJ], wsv[NJ], thp[NJ];
+  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], thp[NJ];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
     const int j = lane + 64 * k;
@@ -916,12 +991,6 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     hi[k] = in ? st.upper[c * ld + j] : 0.0;
     mu[k] = in ? st.pmu[c * ld + j] : 0.0;
     sg[k] = in ? st.psig[c * ld + j] : 0.0;
-    smn[k] = sm2[k] = wsv[k] = 0.0;
-    if (w == kRecWave && in) {  // the record wave keeps the posterior Welford statistics and window sums
-      smn[k] = st.smean[c * ld + j];
-      sm2[k] = st.sm2[c * ld + j];
-      wsv[k] = st.wsumv[c * ld + j];
-    }
   }
   EvalIn<RPL> e;  // the chain's cell records stay in registers
   {
@@ -932,11 +1001,9 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   // (1/(Gl*(2/ss)), ss of the state after the row) is pending; s2 of the first of two rows
   double s2c = st.sigma2[c], Gl = 0.0, s2first = 0.0;
   bool gpend = false;
-  S2Stats s2a{0.0, 0.0, 0.0};
-  if (w == kSigWave) s2a = S2Stats{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
   int32_t nacc = st.naccept[c], nrej = st.nrej_win[c];
   int64_t nev = st.nevals[c];
-  int64_t prow = 0;  // rows prow .. prow + padv - 1 were decided by the previous round (records pending);
+  int64_t prow = 0;  // rows prow .. prow + padv - 1 were decided by the previous round (logs pending);
   int padv = 0;      // of two, the first did not move the chain (its row is thp)
   // Loads one round ahead. The next round starts at step s + 1 or s + 2, so a round loads both
   // candidates at its START (this wave's offsets of rows s + ahead + 1 and s + ahead + 2, and the
@@ -958,27 +1025,56 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   double dsc = load_sc(s_begin), dscn = 0.0;
   int sbase = 0;  // lane of step s's first scalar draw in dsc (0 or 4)
   int par = 0;
-  RowCursor cur;
-  cur.init(p, s_begin);
-  // the records of the pending rows (kRecWave: vectors, kSigWave: s2 with x0 = s2 of the last row)
-  auto flush_vec = [&]() {
-    if (padv == 2) {
-      record_vec_reg<NJ>(st, p, c, prow, P, thp, smn, sm2, wsv, lane, cur);
-      cur.next(p);
+  // the logs of the pending rows (kRecWave: the rows, kSigWave: s2 with x0 = s2 of the last row);
+  // slots are consecutive within a chunk (log_slot)
+  const int64_t slot0 = log_slot(p, s_begin) - s_begin;  // slot of row r: slot0 + r
+  // the window records of the rows as they are decided ("Chain records"): kRecWave's column sums,
+  // kSigWave's s2 sums (lane 0), continuing a window begun by an earlier chunk (or by k_init_stats)
+  ColAcc<NJ> ca;
+  ca.setup(p, s_begin);
+  S2Acc qa{0.0, 0.0, 0.0, 0.0};
+  const bool cont = s_begin != ca.first;
+  if (w == kRecWave) {
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      const int j = lane + 64 * k;
+      const bool in = j < P;
+      ca.ws[k] = cont && in ? st.wsumv[c * ld + j] : 0.0;
+      ca.S1[k] = cont && in ? st.wacc1[c * ld + j] : 0.0;
+      ca.S2[k] = cont && in ? st.wacc2[c * ld + j] : 0.0;
+      ca.K[k] = !in ? 0.0 : !ca.kfirst ? st.smean[c * ld + j] : cont ? st.window[c * p.win * ld + j] : 0.0;
     }
-    if (padv >= 1) {
-      record_vec_reg<NJ>(st, p, c, prow + padv - 1, P, th, smn, sm2, wsv, lane, cur);
-      cur.next(p);
+  }
+  if (w == kSigWave) {
+    qa.sum = cont ? st.s2acc[3 * c + 0] : 0.0;
+    qa.S1 = cont ? st.s2acc[3 * c + 1] : 0.0;
+    qa.S2 = cont ? st.s2acc[3 * c + 2] : 0.0;
+    qa.K = ca.first > 1 ? st.sq_mean[c] : sqrt(st.s2log[c * p.win]);
+  }
+  auto rec_row = [&](int64_t row, const double* x) {
+    log_row<NJ>(st, p, c, slot0 + row, P, x, lane);
+    ca.add(row, x);
+    int64_t k;
+    if (st.chain_out != nullptr && kept_row(p, row, k)) {
+#pragma unroll
+      for (int q = 0; q < NJ; ++q)
+        if (lane + 64 * q < P) st.chain_out[(k * st.n_chains + c) * ld + lane + 64 * q] = x[q];
     }
   };
+  auto rec_s2 = [&](int64_t row, double v) {  // lane 0
+    log_s2(st, p, c, slot0 + row, v);
+    qa.add(v);
+    int64_t k;
+    if (st.s2_out != nullptr && kept_row(p, row, k)) st.s2_out[k * st.n_chains + c] = v;
+  };
+  auto flush_vec = [&]() {
+    if (padv == 2) rec_row(prow, thp);
+    if (padv >= 1) rec_row(prow + padv - 1, th);
+  };
   auto flush_s2 = [&](double x0) {
-    if (padv == 2) {
-      if (lane == 0) record_s2_cur(st, p, c, prow, s2first, s2a, cur);
-      cur.next(p);
-    }
-    if (padv >= 1) {
-      if (lane == 0) record_s2_cur(st, p, c, prow + padv - 1, x0, s2a, cur);
-      cur.next(p);
+    if (lane == 0) {
+      if (padv == 2) rec_s2(prow, s2first);
+      if (padv >= 1) rec_s2(prow + padv - 1, x0);
     }
   };
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = stamp(), t1;
@@ -1141,12 +1237,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
       const int j = lane + 64 * k;
-      if (j < P) {
-        st.theta[c * ld + j] = th[k];
-        st.smean[c * ld + j] = smn[k];
-        st.sm2[c * ld + j] = sm2[k];
-        st.wsumv[c * ld + j] = wsv[k];
-      }
+      if (j < P) st.theta[c * ld + j] = th[k];
     }
     if (lane == 0) {
       st.ss[c] = ss;
@@ -1156,15 +1247,32 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       st.nevals[c] = nev;
       if (c == 0) *st.step = s_end;  // the adaptation reads the row it follows
     }
+    if (with_records) {  // the chunk ends a window (or the run): its records
+      ca.finish(st, p, c, s_end, P, lane);
+    } else {  // the window goes on in the next chunk
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) {
+        const int j = lane + 64 * k;
+        if (j < P) {
+          st.wsumv[c * ld + j] = ca.ws[k];
+          st.wacc1[c * ld + j] = ca.S1[k];
+          st.wacc2[c * ld + j] = ca.S2[k];
+        }
+      }
+    }
   }
   if (w == kSigWave) {
     const double x0 = (p.updatesigma && gpend) ? 1.0 / (Gl * (2.0 / ss)) : s2c;
     flush_s2(x0);
     if (lane == 0) {
       st.sigma2[c] = x0;
-      st.s2sum[c] = s2a.sum;
-      st.sq_mean[c] = s2a.qmean;
-      st.sq_m2[c] = s2a.qm2;
+      if (with_records) {
+        qa.finish(st, c, ca.first, s_end);
+      } else {
+        st.s2acc[3 * c + 0] = qa.sum;
+        st.s2acc[3 * c + 1] = qa.S1;
+        st.s2acc[3 * c + 2] = qa.S2;
+      }
     }
   }
 }
@@ -1177,15 +1285,14 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 // Register budget: two waves per SIMD (229 -> 188 us per config-4 step).
 template <int RPL, int NSEG>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_walk(DramState st, DramParams p, KParams kp, int64_t s_begin,
-                                                                int64_t s_end) {
+                                                                int64_t s_end, int with_records) {
   constexpr int NJ = RPL + 1;
   constexpr int EV = eval_lds_doubles<RPL>();
   constexpr int NW = kThreads / 64;
   __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each wave's {K,J} tables / rows
   __shared__ double yl[NW][64 * NJ];                            // each wave's proposal (theta broadcast)
-  __shared__ double rec[NW][3][64 * NJ];                        // posterior Welford mean / M2, window sums
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int lane = threadIdx.x & 63;  // re-laundered every step (TCI_LOOP_LAUNDER)
+  int lane = threadIdx.x & 63;  // re-laundered every step (launder_lane)
   const int64_t c = (int64_t)blockIdx.x * NW + w;
   if (c >= st.n_chains) return;  // uniform per wave; no workgroup barriers below
   const int64_t ld = st.ld;
@@ -1198,9 +1305,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   // the 2-waves/SIMD budget (config 5: 230 -> 206 ms per 1000 steps; config 4 unchanged).
   constexpr bool kGB = NSEG >= 2;
   double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ];
-  double* smn = &rec[w][0][lane];  // entry k at [64 k] (record_vec_reg<NJ, 64>)
-  double* sm2 = &rec[w][1][lane];
-  double* wsv = &rec[w][2][lane];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
     const int j = lane + 64 * k;
@@ -1212,19 +1316,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
       mu[k] = in ? st.pmu[c * ld + j] : 0.0;
       sg[k] = in ? st.psig[c * ld + j] : 0.0;
     }
-    smn[64 * k] = in ? st.smean[c * ld + j] : 0.0;
-    sm2[64 * k] = in ? st.sm2[c * ld + j] : 0.0;
-    wsv[64 * k] = in ? st.wsumv[c * ld + j] : 0.0;
   }
   EvalIn<RPL> e;  // the chain's cell records stay in registers
   {
     load_cell<RPL, false>(kp, st.cell[c], lane, e);
   }
   double ss = st.ss[c], prior = st.prior[c], s2 = st.sigma2[c];
-  S2Stats s2a{st.s2sum[c], st.sq_mean[c], st.sq_m2[c]};
   int32_t nacc = st.naccept[c], nrej = st.nrej_win[c];
   int64_t nev = st.nevals[c];
   double* yb = yl[w];
+  const int64_t slot0 = log_slot(p, s_begin) - s_begin;  // log slot of row s: slot0 + s
   // ssfun and prior of the proposal th + scale * u (k_chain's per-wave evaluation); an in-bounds
   // proposal is left in yb (a move copies it from there)
   auto evaluate = [&](const double* u, double scale, double& r, double& pr) {
@@ -1268,8 +1369,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     pr = wave_prior_reg<NJ>(y, mu, sg, P, lane);
     return true;
   };
-  RowCursor cur;
-  cur.init(p, s_begin);
   // the row's proposal offsets of one stage (loaded when needed: registers, not prefetch, are short)
   auto load_u = [&](double* u, int64_t s, int stage) {
     const double* src = drow + s * DW + stage * ld;
@@ -1315,19 +1414,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     // sigma2 Gibbs update of this row (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/ss)
     if (p.updatesigma) s2 = 1.0 / (G * (2.0 / ss));
     wave_sync();  // yb reads are done before the next evaluation rewrites it
-    record_vec_reg<NJ, 64>(st, p, c, s, P, th, smn, sm2, wsv, lane, cur);
-    if (lane == 0) record_s2_cur(st, p, c, s, s2, s2a, cur);
-    cur.next(p);
+    log_row<NJ>(st, p, c, slot0 + s, P, th, lane);  // the row's records: k_stats, after the chunk
+    if (lane == 0) log_s2(st, p, c, slot0 + s, s2);
   }
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
     const int j = lane + 64 * k;
-    if (j < P) {
-      st.theta[c * ld + j] = th[k];
-      st.smean[c * ld + j] = smn[64 * k];
-      st.sm2[c * ld + j] = sm2[64 * k];
-      st.wsumv[c * ld + j] = wsv[64 * k];
-    }
+    if (j < P) st.theta[c * ld + j] = th[k];
   }
   if (lane == 0) {
     st.ss[c] = ss;
@@ -1336,10 +1429,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     st.naccept[c] = nacc;
     st.nrej_win[c] = nrej;
     st.nevals[c] = nev;
-    st.s2sum[c] = s2a.sum;
-    st.sq_mean[c] = s2a.qmean;
-    st.sq_m2[c] = s2a.qm2;
     if (c == 0) *st.step = s_end;  // the adaptation reads the row it follows
+  }
+  if (with_records) {  // the chunk ends a window (or the run): its records, from the logs just written
+    __threadfence_block();  // lane 0's s2 logs before the other lanes read them
+    window_records(st, p, c, s_end, lane);
   }
 }
 
@@ -1352,33 +1446,36 @@ inline int draws_ct(int64_t ld, int nwd) {
 
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
-                   hipStream_t stream) {
+                   int with_records, hipStream_t stream) {
   const size_t lds = (size_t)draws_lds_bytes(st.ld);
-  const int ct = draws_ct(st.ld, p.walk ? 8 : 4);
-  auto kd = p.walk ? (ct <= 2 ? k_draws<8, 2> : k_draws<8, 3>)
-                   : (ct <= 2 ? k_draws<4, 2> : ct <= 3 ? k_draws<4, 3> : k_draws<4, 5>);
+  // 8-wave workgroups once one workgroup fills a CU's LDS (WALK: P = 207; FUSED: P > ~100 with R in
+  // FP64), 4-wave ones while two share a CU
+  const int nwd = p.walk || lds > 80 * 1024 ? 8 : 4;
+  const int ct = draws_ct(st.ld, nwd);
+  auto kd = nwd == 8 ? (ct <= 2 ? k_draws<8, 2> : k_draws<8, 3>)
+                     : (ct <= 2 ? k_draws<4, 2> : ct <= 3 ? k_draws<4, 3> : k_draws<4, 5>);
   if (ensure_dyn_lds((const void*)kd, lds) != TCI_OK) return TCI_EHIP;
   const int npass = draws_passes(st.ld, p.walk != 0);
   const int64_t per_wg = (int64_t)kDrawSteps * npass;  // <= the workgroup's threads (scalar draws)
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
-  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(p.walk ? 512 : 256), lds, stream, st, p, s_begin, s_end,
-                     npass);
+  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(64 * nwd), lds, stream, st, p, s_begin, s_end, npass);
   if (p.walk)
     hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, stream, st, p,
-                       kp, s_begin, s_end);
+                       kp, s_begin, s_end, with_records);
   else
     hipLaunchKernelGGL((k_chain<RPL, NSEG>), dim3((unsigned)st.n_chains), dim3(kThreads), 0, stream, st, p, kp,
-                       s_begin, s_end);
+                       s_begin, s_end, with_records);
   return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;
 }
 
 template <int RPL>
-int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, int64_t a, int64_t b, hipStream_t s) {
+int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, int64_t a, int64_t b, int rec,
+                   hipStream_t s) {
   switch (kp.n_seg) {
-    case 1: return launch_chain_t<RPL, 1>(st, p, kp, a, b, s);
-    case 2: return launch_chain_t<RPL, 2>(st, p, kp, a, b, s);
-    case 3: return launch_chain_t<RPL, 3>(st, p, kp, a, b, s);
-    case 4: return launch_chain_t<RPL, 4>(st, p, kp, a, b, s);
+    case 1: return launch_chain_t<RPL, 1>(st, p, kp, a, b, rec, s);
+    case 2: return launch_chain_t<RPL, 2>(st, p, kp, a, b, rec, s);
+    case 3: return launch_chain_t<RPL, 3>(st, p, kp, a, b, rec, s);
+    case 4: return launch_chain_t<RPL, 4>(st, p, kp, a, b, rec, s);
     default: return TCI_EINVAL;
   }
 }
@@ -1396,6 +1493,22 @@ __device__ __forceinline__ double row_bcast16(double x) {
   return __hiloint2double(hi, lo);
 }
 
+// 16-lane row G's x in every row (lane l gets lane 16 G + (l & 15)): two gfx950 permlane swaps per
+// 32-bit half (permlane32_swap pairs rows {0,1} with {2,3}, permlane16_swap row 0 with 1 and 2
+// with 3), no LDS round trip (ds_bpermute waits on the LDS pipe).
+template <int G>
+__device__ __forceinline__ double row_to_all(double x) {
+  unsigned h[2] = {(unsigned)__double2loint(x), (unsigned)__double2hiint(x)};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const auto a = __builtin_amdgcn_permlane32_swap(h[q], h[q], false, false);  // [R0 R1 R0 R1], [R2 R3 R2 R3]
+    const unsigned y = G < 2 ? a[0] : a[1];
+    const auto b = __builtin_amdgcn_permlane16_swap(y, y, false, false);        // [Ra Ra Ra Ra], [Rb Rb Rb Rb]
+    h[q] = (G & 1) ? b[1] : b[0];
+  }
+  return __hiloint2double((int)h[1], (int)h[0]);
+}
+
 // Step K of the Cholesky factorization A = U'U of a symmetric 16 x 16 tile held by ONE wave in
 // registers, in the MFMA accumulator layout (lane 16 g + j holds rows g, g+4, g+8, g+12 of
 // column j). Rows and columns > K take the symmetric rank-1 update A -= a_K a_K' / d (both
@@ -1411,7 +1524,7 @@ __device__ __forceinline__ void chol16_step(double (&a)[4], int lane, double* dp
     bad = bad || !(d > 0.0) || !isfinite(d);
     double rd = __builtin_amdgcn_rcp(d);
     rd = fma(rd, fma(-d, rd, 1.0), rd);
-    const double akj = __shfl(a[kr], 16 * kg + j);  // A[K][j]
+    const double akj = row_to_all<kg>(a[kr]);  // A[K][j]
     double aik[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) aik[q] = row_bcast16<K>(a[q]);  // A[g + 4q][K]
@@ -1492,7 +1605,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8
   double* cvg = st.cov + c * ld * ld;
   double* mu = st.cmean + c * ld;
   const int nb = (TCI_ADAPT_ABLATE & 2) ? 0 : (int)p.adaptint;
-  const double* win = st.window + c * p.adaptint * ld;
+  const double* win = st.window + c * p.win * ld;
   uint64_t aph[6] = {0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
 #define TCI_APHASE(k) \
   if (TCI_ADAPT_PROFILE) { a1 = stamp(); aph[k] += a1 - a0; a0 = a1; }
@@ -1704,7 +1817,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int i = 16 * sti[o] + kq + 4 * q, j = 16 * stj[o] + row;
-        if (i < P && j < P && j >= i) store_R(st, c, P, i, j, f32_round(acc[o][q] * sc));
+        if (i < P && j < P && j >= i) store_R(st, c, P, i, j, acc[o][q] * sc);
       }
     }
   }
@@ -1782,7 +1895,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
   double* Wt = st.work + c * LT * LT;
   auto tile = [&](int ti, int tj) { return Wt + ((int64_t)ti * NT + tj) * 256; };
   const int nb = (int)p.adaptint;
-  const double* win = st.window + c * p.adaptint * ld;
+  const double* win = st.window + c * p.win * ld;
   // TCI_ADAPT_PROFILE: thread 0's s_memtime cycles per phase: scatter, merge, diagonal tiles,
   // panel solves, trailing updates, R store
   uint64_t aph[6] = {0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
@@ -2025,7 +2138,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int i = 16 * tis[g] + kq + 4 * q, j = 16 * tjs[g] + row;
-          if (i < P && j < P && j >= i) store_R(st, c, P, i, j, f32_round(a[g][q] * sc));
+          if (i < P && j < P && j >= i) store_R(st, c, P, i, j, a[g][q] * sc);
         }
       }
     }
@@ -2086,19 +2199,23 @@ int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
   return finish();
 }
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,
-                      int64_t s_end, void* stream) {
+                      int64_t s_end, int with_records, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   switch (rpl) {
-    case 1: return launch_chain_r<1>(st, p, kp, s_begin, s_end, s);
-    case 2: return launch_chain_r<2>(st, p, kp, s_begin, s_end, s);
-    case 4: return launch_chain_r<4>(st, p, kp, s_begin, s_end, s);
-    case 8: return launch_chain_r<8>(st, p, kp, s_begin, s_end, s);
+    case 1: return launch_chain_r<1>(st, p, kp, s_begin, s_end, with_records, s);
+    case 2: return launch_chain_r<2>(st, p, kp, s_begin, s_end, with_records, s);
+    case 4: return launch_chain_r<4>(st, p, kp, s_begin, s_end, with_records, s);
+    case 8: return launch_chain_r<8>(st, p, kp, s_begin, s_end, with_records, s);
     default: return TCI_EINVAL;
   }
 }
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl) {
   const int64_t chain = (4 * (4 * 64 * rpl + 4 * rpl) + 2 * 4 * 64 * (rpl + 1) + 2 * 4 * 4 + 2 * 2 * 5) * 8;  // k_chain
   return std::max<int64_t>(chain, draws_lds_bytes(ld));                                  // k_draws (dynamic)
+}
+int dram_launch_stats(const DramState& st, const DramParams& p, void* stream) {
+  hipLaunchKernelGGL(k_stats, dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, (hipStream_t)stream, st, p);
+  return finish();
 }
 int dram_launch_step_incr(const DramState& st, void* stream) {
   hipLaunchKernelGGL(k_step_incr, dim3(1), dim3(64), 0, (hipStream_t)stream, st.step);

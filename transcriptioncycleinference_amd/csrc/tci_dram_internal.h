@@ -10,9 +10,9 @@ namespace tci {
 
 // One workgroup (256 threads) per chain. All arrays are indexed by chain c; vectors have stride ld (= max parameter count P_max),
 // matrices stride ld*ld (row-major, P_c x P_c used).
-// Floats per chain of DramState::Rf: the packed triangle ld(ld+1)/2 rounded up to 256 floats, so a
+// Doubles per chain of DramState::Rd: the packed triangle ld(ld+1)/2 rounded up to 128 doubles, so a
 // chain's triangle starts 1 KiB-aligned and is copied to LDS in whole 1 KiB pieces (k_draws).
-constexpr int64_t dram_tri_stride(int64_t ld) { return (ld * (ld + 1) / 2 + 255) / 256 * 256; }
+constexpr int64_t dram_tri_stride(int64_t ld) { return (ld * (ld + 1) / 2 + 127) / 128 * 128; }
 
 struct DramState {
   int64_t n_chains;
@@ -29,14 +29,20 @@ struct DramState {
   double* ss;              // SS of the current state
   double* prior;           // prior SS of the current state
   double* sigma2;          // error variance (model.sigma2, :259)
-  float* Rf;               // proposal Cholesky factor R (upper, float-representable: proposal = theta + z * R)
-                           // as packed fp32 upper triangles (chain c at c * dram_tri_stride(ld)); the
+  double* Rd;              // proposal Cholesky factor R (upper: proposal = theta + z * R) in FP64, as packed
+                           // upper triangles (chain c at c * dram_tri_stride(ld)); the
                            // [ld][ld] double form is built on the host for the results only
   double* cov;             // running chain covariance / mean / weight (mcmcstat covupd)
   double* cmean;
   double* wsum;
-  double* window;          // the last adaptint chain rows (for covupd)
-  double* wsumv;           // column sums of the window's rows so far (row order; the adaptation's batch mean)
+  double* window;          // chain rows by window slot (DramParams::win per chain): the covupd window, and
+                           // every engine's per-row log (k_stats)
+  double* s2log;           // s2 of each row of the window, by window slot
+  double* wsumv;           // column sums of the window's rows (row order; the adaptation's batch mean); during a
+                           // window that spans k_chain launches, its running sums so far with
+  double* wacc1;           //   the shifted sums S1, S2 of the statistics rows (n_chains x ld)
+  double* wacc2;
+  double* s2acc;           //   and the s2 sums: sum, S1, S2 per chain (n_chains x 3)
   double* prop1;           // stage-1 / stage-2 proposals (n_chains x ld)
   double* prop2;
   uint8_t* act1;           // in-bounds flags (ssfun is called only for these)
@@ -82,6 +88,8 @@ struct DramParams {
   int64_t pmax;        // max parameter count over the chains (picks the adaptation kernel)
   int64_t chunk;       // fused engine: rows per chain of the draws buffer (>= the longest chunk)
   int64_t walk;        // fused engine: 1 = one wavefront per chain walks the chunk (k_walk), 0 = k_chain
+  int64_t win;         // window rows per chain: adaptint, or (no adaptation) the fused engine's chunk; the
+                       // records are merged window by window (k_stats), the same partition for every engine
 };
 
 int dram_launch_init(const DramState& st, const double* qcov_diag, const double* sigma2_0, void* stream);
@@ -92,8 +100,14 @@ int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream);  
 int dram_launch_step_incr(const DramState& st, void* stream);
 int dram_launch_init_stats(const DramState& st, const DramParams& p, void* stream);
 // Fused engine: chain rows s_begin..s_end (each chain's ssfun inside the kernel); leaves *st.step = s_end.
+// with_records: s_end ends a window (or the run) -- the window's records are kept by the same kernel.
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,
-                      int64_t s_end, void* stream);
+                      int64_t s_end, int with_records, void* stream);
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl);  // LDS per workgroup of the fused engine
+// The records of the window of chain rows ending at row *st.step (posterior mean / M2, window column
+// sums, s2 statistics, thinned outputs) from the rows every engine logs: run after a window's last
+// row (a multiple of p.win) and after the chain's last row (the batched engine; the fused engines
+// keep them in the chain kernel, dram_launch_chain).
+int dram_launch_stats(const DramState& st, const DramParams& p, void* stream);
 
 }  // namespace tci
