@@ -647,33 +647,22 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
 }
 
 #ifndef TCI_DRAWS_ABLATE
-#define TCI_DRAWS_ABLATE 0  // diagnostics only (wrong results): bit0 no normals, bit1 no MFMA, bit2 no scalars, bit3 no R load
+#define TCI_DRAWS_ABLATE 0  // diagnostics only (wrong results): bit0 no normals, bit1 no MFMA, bit2 no scalars
 #endif
-constexpr int kDrawsPF = 2;               // R from global memory: R values prefetched this many k-steps ahead (mfma_zr PF)
+constexpr int kDrawsPF = 2;               // R values prefetched this many k-steps ahead (mfma_zr PF)
 constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each)
 constexpr int kDrawSteps = 8 * kDrawMT;   // steps per pass (2 rows per step)
-constexpr int kDrawPasses = 2;            // passes per k_draws workgroup (32 steps)
-// passes per workgroup when R is read from global memory (past the LDS budget): every workgroup
-// reads the chain's whole R once per pass, so fewer, longer workgroups read it fewer times
-constexpr int kDrawPassesGR = 4;
 enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
 
-// Dynamic LDS of k_draws: one pass's normals (2 x kDrawSteps rows of stride L) and the chain's R
-// as packed FP64 (P <= 150 or so: every TestData cell).
-// R is staged only while it fits beside the normals; longer rows read the packed R from global
-// memory in the same MFMA order (the same bits).
-__host__ __device__ inline bool draws_r_lds(int64_t L) {
-  return (2 * kDrawSteps * L) * 8 + dram_tri_stride(L) * 8 + 16 <= 160 * 1024;
-}
-__host__ __device__ inline int64_t draws_lds_bytes(int64_t L) {
-  return (2 * kDrawSteps * L) * 8 + (draws_r_lds(L) ? dram_tri_stride(L) * 8 : 0) + 16;
-}
-// WALK (thousands of chains, one draws workgroup per CU): passes per workgroup with R in LDS,
-// so R is staged once per 64 steps (configs 4/5: 174.3 -> 171.6 us per step; 7 passes: 171.9)
-constexpr int kDrawPassesWalk = 4;
-__host__ __device__ inline int draws_passes(int64_t ld, bool walk) {
-  return !draws_r_lds(ld) ? kDrawPassesGR : walk ? kDrawPassesWalk : kDrawPasses;
-}
+// Dynamic LDS of k_draws: one pass's normals (2 x kDrawSteps rows of stride L). The chain's packed
+// FP64 R is read from global memory (L2) with a kDrawsPF-deep prefetch: staging it in LDS beside the
+// normals (74 KB at P = 136) left one workgroup per CU, and that layout took 144 us per TestData
+// chunk against 105 us with R from L2 and four 35 KB workgroups per CU (r03n/r03o).
+__host__ __device__ inline int64_t draws_lds_bytes(int64_t L) { return (2 * kDrawSteps * L) * 8 + 16; }
+// Passes per workgroup: every workgroup reads the chain's R once per pass. FUSED (a few hundred
+// chains): 2 (1: 108.8, 2: 104.7, 4: 123.7 us per TestData chunk); WALK (thousands of chains, P =
+// 207): 4, fewer and longer workgroups reading R fewer times.
+__host__ __device__ inline int draws_passes(bool walk) { return walk ? 4 : 2; }
 
 // NWD waves per workgroup: 4 for the FUSED engine (299 TestData chains: 100.6 vs 105.4 ms per 20k
 // steps with 8), 8 for WALK (10,000 chains, one workgroup per CU at P = 207: 175 vs 188 ms per
@@ -695,9 +684,6 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
   const int64_t DW = draw_stride(ld);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   double* Z = dyn;
-  double* Rl = Z + 2 * kDrawSteps * L;
-  const bool rl = draws_r_lds(ld);
-  if (rl && !(TCI_DRAWS_ABLATE & 8)) load_R_glds<kDrawThreads>(Rl, st, c, P);
   const double* Rg = st.Rd + c * tri_stride(ld);
   const double a = 0.5 * (double)st.nobs[c];
   const double inv_ds = 1.0 / p.drscale;
@@ -707,23 +693,13 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
     if (step0 > s_end) break;  // uniform over the workgroup
     const int ns = (int)min<int64_t>(kDrawSteps, s_end - step0 + 1);
     if (!(TCI_DRAWS_ABLATE & 1)) draw_block_normals<kDrawThreads>(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
-    // The first pass also waits for R: an LDS-DMA copy is counted on vmcnt, and a workgroup-scope
-    // barrier need not drain vmcnt, so every wave waits for its own pieces explicitly before the
-    // barrier (as composable_kernel's block_sync_lds_direct_load does). Later passes have no DMA in
-    // flight, only the previous pass's global stores, which they must not wait for.
-    if (pass == 0 && rl) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // (the first pass: also R)
+    __syncthreads();
     // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
     double* d0 = drow + step0 * DW;
-    // R from LDS or global memory: two call sites, so that each inlined copy reads R with the
-    // instructions of its address space (one call through a selected pointer made every R read a
-    // flat load, with global-memory latency, also from LDS)
     const auto put = [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; };
     if (!(TCI_DRAWS_ABLATE & 2))
-      for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT) {
-        if (rl) mfma_zr<kDrawMT, kDrawCT, kDrawWaves>(Z, L, 2 * ns, Rl, P, top, put);
-        else mfma_zr<kDrawMT, kDrawCT, kDrawWaves, decltype(put), kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
-      }
+      for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT)
+        mfma_zr<kDrawMT, kDrawCT, kDrawWaves, decltype(put), kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
     for (int k = w; k < ns; k += kDrawWaves) {
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
       if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
@@ -1448,14 +1424,14 @@ template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    int with_records, hipStream_t stream) {
   const size_t lds = (size_t)draws_lds_bytes(st.ld);
-  // 8-wave workgroups once one workgroup fills a CU's LDS (WALK: P = 207; FUSED: P > ~100 with R in
-  // FP64), 4-wave ones while two share a CU
-  const int nwd = p.walk || lds > 80 * 1024 ? 8 : 4;
+  // 8-wave workgroups for WALK (10,000 chains at P = 207), 4-wave ones for FUSED (TestData: 104.7
+  // against 134.6 us per chunk with 8)
+  const int nwd = p.walk ? 8 : 4;
   const int ct = draws_ct(st.ld, nwd);
   auto kd = nwd == 8 ? (ct <= 2 ? k_draws<8, 2> : k_draws<8, 3>)
                      : (ct <= 2 ? k_draws<4, 2> : ct <= 3 ? k_draws<4, 3> : k_draws<4, 5>);
   if (ensure_dyn_lds((const void*)kd, lds) != TCI_OK) return TCI_EHIP;
-  const int npass = draws_passes(st.ld, p.walk != 0);
+  const int npass = draws_passes(p.walk != 0);
   const int64_t per_wg = (int64_t)kDrawSteps * npass;  // <= the workgroup's threads (scalar draws)
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
   hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(64 * nwd), lds, stream, st, p, s_begin, s_end, npass);
