@@ -48,16 +48,23 @@ constexpr int kThreads = 256;  // one workgroup (4 waves) per chain
 
 enum Purpose : uint32_t { P_NORM1 = 1, P_U1 = 2, P_NORM2 = 3, P_U2 = 4, P_GAMMA = 5 };
 
-__device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
-  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+
+// The 32 x 32 -> 64-bit product of a Philox round in one v_mad_u64_u32: the compiler's
+// v_mul_lo_u32 + v_mul_hi_u32 pair is two quarter-rate instructions (draws pass: TestData 105.0 ->
+// 97.5 us per chunk, config 4 62.1 -> 52.7 ms per 1,000 steps, r03v; the same exact product).
+__device__ __forceinline__ uint64_t mul64(uint32_t a, uint32_t b) {
+  uint64_t r, carry;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(carry) : "v"(a), "v"(b));
+  return r;
 }
 
 // Philox4x32-10 (Salmon et al. 2011).
 __device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = mulhi32(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi1 = mulhi32(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    const uint64_t p0 = mul64(0xD2511F53u, c.x), p1 = mul64(0xCD9E8D57u, c.z);
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
     k.x += 0x9E3779B9u;
     k.y += 0xBB67AE85u;
@@ -664,12 +671,9 @@ __host__ __device__ inline int64_t draws_lds_bytes(int64_t L) { return (2 * kDra
 // 207): 4, fewer and longer workgroups reading R fewer times.
 __host__ __device__ inline int draws_passes(bool walk) { return walk ? 4 : 2; }
 
-// NWD waves per workgroup: 4 for the FUSED engine (299 TestData chains: 100.6 vs 105.4 ms per 20k
-// steps with 8), 8 for WALK (10,000 chains, one workgroup per CU at P = 207: 175 vs 188 ms per
-// 1000 steps with 4). CT column tiles per wave and MFMA call: the smallest CT whose NWD*CT tiles
-// cover the row (draws_ct), since the accumulators of CT*2 tiles set the register count and with
-// it the waves per SIMD; longer rows loop over calls. The wave count and CT only move column
-// tiles between waves and calls: same bits.
+// NWD waves per workgroup, CT column tiles per wave and MFMA call (launch_chain_t: 4 and 2); longer
+// rows loop over calls. The wave count and CT only move column tiles between waves and calls: same
+// bits.
 template <int NWD, int CT>
 __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end, int npass) {
   constexpr int kDrawWaves = NWD, kDrawThreads = 64 * NWD;
@@ -1413,28 +1417,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   }
 }
 
-// Column tiles per wave of k_draws: the row's 16-column tiles over the waves, at most 5 (4 waves)
-// or 3 (8 waves) per call.
-inline int draws_ct(int64_t ld, int nwd) {
-  const int64_t tiles = (ld + 15) / 16, per = (tiles + nwd - 1) / nwd;
-  return (int)std::min<int64_t>(per < 2 ? 2 : per, nwd == 8 ? 3 : 5);
-}
-
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    int with_records, hipStream_t stream) {
   const size_t lds = (size_t)draws_lds_bytes(st.ld);
-  // 8-wave workgroups for WALK (10,000 chains at P = 207), 4-wave ones for FUSED (TestData: 104.7
-  // against 134.6 us per chunk with 8)
-  const int nwd = p.walk ? 8 : 4;
-  const int ct = draws_ct(st.ld, nwd);
-  auto kd = nwd == 8 ? (ct <= 2 ? k_draws<8, 2> : k_draws<8, 3>)
-                     : (ct <= 2 ? k_draws<4, 2> : ct <= 3 ? k_draws<4, 3> : k_draws<4, 5>);
+  // 4-wave workgroups, 2 column tiles x 2 row tiles per wave and MFMA call (164 VGPRs: three
+  // workgroups per CU). Config 4 (WALK, P = 207): 72.7 ms per 1,000 steps with the 8-wave, 2-tile
+  // form -> 53.6 (3 tiles: 58.0, 5: 56.4); TestData (FUSED): 105.3 -> 99.8 us per chunk against
+  // 3 tiles (r03t4, r03u).
+  auto kd = k_draws<4, 2>;
   if (ensure_dyn_lds((const void*)kd, lds) != TCI_OK) return TCI_EHIP;
   const int npass = draws_passes(p.walk != 0);
   const int64_t per_wg = (int64_t)kDrawSteps * npass;  // <= the workgroup's threads (scalar draws)
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
-  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(64 * nwd), lds, stream, st, p, s_begin, s_end, npass);
+  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(64 * 4), lds, stream, st, p, s_begin, s_end, npass);
   if (p.walk)
     hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, stream, st, p,
                        kp, s_begin, s_end, with_records);

@@ -53,10 +53,28 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
   e.b2 = th[4];
   e.A = th[5];
   e.R = th[6];
+  if (RPL >= 2) {
+    // dR pairs (8-B aligned 16-B loads): one load instruction per two entries where the pair is
+    // inside the row, entry by entry at the row's end (41.8 vs 42.3 us per bench launch, r03t)
+    typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
 #pragma unroll
-  for (int q = 0; q < RPL; ++q) {
-    const int g = RPL * lane + q;
-    e.dr[q] = 7 + g < ld ? th[7 + g] : 0.0;  // speculative (N unknown yet), kept inside the row
+    for (int q = 0; q < RPL; q += 2) {
+      const int g = RPL * lane + q;
+      if (8 + g < ld) {
+        const d2u x = *reinterpret_cast<const d2u*>(th + 7 + g);
+        e.dr[q] = x.x;
+        e.dr[q + 1] = x.y;
+      } else {
+        e.dr[q] = 7 + g < ld ? th[7 + g] : 0.0;
+        e.dr[q + 1] = 0.0;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < RPL; ++q) {
+      const int g = RPL * lane + q;
+      e.dr[q] = 7 + g < ld ? th[7 + g] : 0.0;  // speculative (N unknown yet), kept inside the row
+    }
   }
   const int N = e.cm.n;
   if (ld < 7 + N) {  // a row shorter than 7 + N entries
