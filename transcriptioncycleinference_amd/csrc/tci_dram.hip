@@ -924,32 +924,50 @@ constexpr int kRecWave = 0, kSigWave = 2;  // (six placements measured within 1 
 // spill at RPL = 4 (config 5: 199.7 -> 191-193 us per step) and trims k_chain<2,1>'s SGPR spill.
 __device__ __forceinline__ void launder_lane(int& lane) { asm volatile("" : "+v"(lane)); }
 
-template <int RPL, int NSEG>
+// Evaluations per wave and round of k_chain: EPW = 1 speculates 2 steps per round, EPW = 2 four
+// (each wave evaluates its stage's proposals of two steps, one after the other). EPW = 2 decides
+// 3.02 steps per round instead of 1.82 on the 299 TestData chains, but its rounds are ~1.75x as
+// long and the 43 CUs that hold two chains become the long pole: k_chain 411 vs 260 us per 100
+// steps (r03y). Only EPW = 1 is instantiated; the EPW = 2 instance was bitwise equal to the other
+// engines (tests/test_dram_gpu.py green with it).
+constexpr int kChainEPW = 1;
+template <int RPL, int NSEG, int EPW>
 __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
                                                     int64_t s_end, int with_records) {
   // Round structure (one workgroup barrier per round). At the start of a round the state after
-  // row s-1 is known. Wave w evaluates proposal (stage w&1) of step s + (w>>1): waves 0/1 the
-  // stage-1/2 proposals of step s, waves 2/3 those of step s+1 drawn around the SAME state, i.e.
-  // speculating that step s does not move the chain (the common case: mcmcstat's DRAM accepts a
-  // minority of steps). After the barrier every wave takes step s's decisions; when the chain did
-  // not move, step s+1's evaluations are exactly the ones the sequential sampler would make, and
-  // step s+1 is decided in the same round. Decisions, counters and records are those of the
-  // step-by-step sampler (and of the batched engine) bit for bit.
+  // row s-1 is known. The round speculates D = 2 EPW steps: proposal slot 2h + stage holds the
+  // stage-1/2 proposal of step s + h, drawn around the SAME state, i.e. speculating that steps
+  // s .. s + h - 1 do not move the chain (the common case: mcmcstat's DRAM accepts a minority of
+  // steps). Wave w evaluates its stage (w & 1) of steps s + (w >> 1) + 2e, e < EPW. After the
+  // barrier every wave takes the decisions of steps s, s + 1, .. from the exchanged values until
+  // one moves the chain: up to D steps are decided per round, each exactly as the step-by-step
+  // sampler (and the batched engine) decides it, bit for bit.
   //
   // After the barrier only the decisions run: one lane-parallel exp and the compares. Everything
   // that does not depend on the exchanged values happens before the barrier, on the stage-1
   // waves (kRecWave, kSigWave), one round late for the records:
-  //   * the precisions the decisions use: 1/s2 of the current state (step s) and, for step s+1
-  //     after an unmoved step s, 1/s2 with s2 = 1/(G_s*(2/ss)) -- both known before the round;
+  //   * the precisions the decisions use: 1/s2 of the current state (step s) and, for step s + h
+  //     after unmoved steps s .. s + h - 1, 1/s2 with s2 = 1/(G_{s+h-1}*(2/ss)) -- known before
+  //     the round;
   //   * the s2 of the rows the previous round decided (1/(G*(2/ss)) of the state after them)
-  //     and the logs of those rows (k_stats turns them into the records after the chunk).
+  //     and the logs and window sums of those rows.
   constexpr int NJ = RPL + 1;  // vector entries per lane: P = 7 + N <= 64 RPL + 8 <= 64 NJ
   constexpr int EV = eval_lds_doubles<RPL>();
   constexpr int NW = kThreads / 64;
+  constexpr int D = 2 * EPW;                // steps per round
+  constexpr int NS = 2 * D;                 // proposal slots
+  // candidate rows for the next round: row s + a1 + 1 + k for k < NC. EPW = 1: both (k = 0, 1);
+  // EPW = 2: the rows of an advance by 1 or 4 (k = 0, 2, 3, 5) -- an advance by 2 or 3 loads its
+  // missing row (k = 1 or 4) after the decisions: six prefetched rows exceeded the 256-register
+  // budget of two chains per CU
+  constexpr int NC = D + 2 * (EPW - 1);
+  constexpr int NPF = EPW == 1 ? 2 : 4;
+  constexpr int kPf[4] = {0, EPW == 1 ? 1 : 2, 3, 5};  // prefetched k (the first NPF)
+  constexpr int NSC = 4 * (2 * D - 1);      // lanes of scalar draws: rows s + 1 .. s + 2D - 1
   __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each evaluating wave's tables
-  __shared__ double yl[2][NW][64 * NJ];                         // by round parity: each wave's proposal
-  __shared__ double xch[2][NW][4];                              // by round parity: ss, prior, in-bounds of each
-  __shared__ double xip[2][2];                                  // by round parity: the precisions of steps s, s+1
+  __shared__ double yl[2][NS][64 * NJ];                         // by round parity: every proposal
+  __shared__ double xch[2][NS][4];                              // by round parity: ss, prior, in-bounds
+  __shared__ double xip[2][D];                                  // by round parity: precisions of steps s + h
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -958,7 +976,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   const int P = st.npar[c];
   const int64_t DW = draw_stride(ld);
   const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
-  const int stage = w & 1, ahead = w >> 1;                        // this wave's proposal
+  const int stage = w & 1, a1 = w >> 1;                           // this wave's slots: steps s + a1 + 2e
   const double scale = stage ? 1.0 / p.drscale : 1.0;
   double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], thp[NJ];
 #pragma unroll
@@ -978,38 +996,39 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   }
   double ss = st.ss[c], prior = st.prior[c];
   // sigma2 chain (kSigWave): s2 of the last decided row, or its Gamma variate Gl while that s2
-  // (1/(Gl*(2/ss)), ss of the state after the row) is pending; s2 of the first of two rows
-  double s2c = st.sigma2[c], Gl = 0.0, s2first = 0.0;
+  // (1/(Gl*(2/ss)), ss of the state after the row) is pending; s2f[i]: s2 of row s + i if the
+  // round's steps s .. s + i do not move the chain
+  double s2c = st.sigma2[c], Gl = 0.0, s2f[D - 1];
+#pragma unroll
+  for (int i = 0; i < D - 1; ++i) s2f[i] = 0.0;
   bool gpend = false;
   int32_t nacc = st.naccept[c], nrej = st.nrej_win[c];
   int64_t nev = st.nevals[c];
   int64_t prow = 0;  // rows prow .. prow + padv - 1 were decided by the previous round (logs pending);
-  int padv = 0;      // of two, the first did not move the chain (its row is thp)
-  // Loads one round ahead. The next round starts at step s + 1 or s + 2, so a round loads both
-  // candidates at its START (this wave's offsets of rows s + ahead + 1 and s + ahead + 2, and the
-  // scalar draws of rows s + 1 .. s + 3) and the next round picks one: a whole round hides the
-  // latency. (Loads issued at the end of the round were waited for at the loop back-edge, where
-  // the rotation of the prefetch registers needs their data: ~2-5 k cycles a round.) The scalar
-  // draws are vector loads (lane j: row r0 + j / 4, slot j % 4) read by readlane: scalar loads
-  // would also be waited for at the evaluation's first LDS wait.
+  int padv = 0;      // all but the last did not move the chain (their state is thp)
+  // Loads one round ahead. The next round starts at step s + 1 .. s + D, so a round loads every
+  // candidate at its START (this wave's offsets of rows s + a1 + 1 .. s + a1 + NC, and the scalar
+  // draws of rows s + 1 .. s + 2D - 1) and the next round picks its rows: a whole round hides the
+  // latency. The scalar draws are vector loads (lane j: row r0 + j / 4, slot j % 4) read by
+  // readlane: scalar loads would also be waited for at the evaluation's first LDS wait.
   auto load_u = [&](double* u, int64_t row) {
     const double* src = drow + min(row, s_end) * DW + stage * ld;
 #pragma unroll
     for (int k = 0; k < NJ; ++k) u[k] = lane + 64 * k < P ? src[lane + 64 * k] : 0.0;
   };
   auto load_sc = [&](int64_t r0) {
-    return lane < 12 ? drow[min(r0 + (lane >> 2), s_end) * DW + 2 * ld + (lane & 3)] : 0.0;
+    return lane < NSC ? drow[min(r0 + (lane >> 2), s_end) * DW + 2 * ld + (lane & 3)] : 0.0;
   };
-  double ucur[NJ], un1[NJ], un2[NJ];
-  load_u(ucur, s_begin + ahead);
+  double ucur[EPW][NJ], cand[NPF][NJ];
+#pragma unroll
+  for (int q = 0; q < EPW; ++q) load_u(ucur[q], s_begin + a1 + 2 * q);
   double dsc = load_sc(s_begin), dscn = 0.0;
-  int sbase = 0;  // lane of step s's first scalar draw in dsc (0 or 4)
+  int sbase = 0;  // lane of step s's first scalar draw in dsc (4 (adv - 1) of the previous round)
   int par = 0;
-  // the logs of the pending rows (kRecWave: the rows, kSigWave: s2 with x0 = s2 of the last row);
-  // slots are consecutive within a chunk (log_slot)
+  // the logs and window sums of the rows as they are decided ("Chain records"): kRecWave's column
+  // sums, kSigWave's s2 sums (lane 0), continuing a window begun by an earlier chunk (or by
+  // k_init_stats); slots are consecutive within a chunk (log_slot)
   const int64_t slot0 = log_slot(p, s_begin) - s_begin;  // slot of row r: slot0 + r
-  // the window records of the rows as they are decided ("Chain records"): kRecWave's column sums,
-  // kSigWave's s2 sums (lane 0), continuing a window begun by an earlier chunk (or by k_init_stats)
   ColAcc<NJ> ca;
   ca.setup(p, s_begin);
   S2Acc qa{0.0, 0.0, 0.0, 0.0};
@@ -1047,13 +1066,18 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     int64_t k;
     if (st.s2_out != nullptr && kept_row(p, row, k)) st.s2_out[k * st.n_chains + c] = v;
   };
-  auto flush_vec = [&]() {
-    if (padv == 2) rec_row(prow, thp);
+  auto flush_vec = [&]() {  // unrolled: a bounded store count (a runtime loop made the compiler
+                            // wait for every store before the next round's loads were used)
+#pragma unroll
+    for (int i = 0; i < D - 1; ++i)
+      if (i + 1 < padv) rec_row(prow + i, thp);  // uniform
     if (padv >= 1) rec_row(prow + padv - 1, th);
   };
   auto flush_s2 = [&](double x0) {
     if (lane == 0) {
-      if (padv == 2) rec_s2(prow, s2first);
+#pragma unroll
+      for (int i = 0; i < D - 1; ++i)
+        if (i + 1 < padv) rec_s2(prow + i, s2f[i]);
       if (padv >= 1) rec_s2(prow + padv - 1, x0);
     }
   };
@@ -1062,66 +1086,73 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   if (TCI_CHAIN_PROFILE) { t1 = stamp(); ph[k] += t1 - t0; t0 = t1; }
   for (int64_t s = s_begin; s <= s_end; par ^= 1) {
     launder_lane(lane);
-    const bool has_next = s + 1 <= s_end;
-    // the scalar draws of steps s and s+1 (loaded by the previous round; dsc lane sbase + 4 h + slot)
-    // are broadcast where they are used, so no scalar copy lives across the evaluation
-    // ---- this wave's proposal and its bounds (wave vote)
-    double y[NJ];
-    bool out = false;
+    // ---- this wave's proposals, their bounds (wave vote) and evaluations
 #pragma unroll
-    for (int k = 0; k < NJ; ++k) {
-      y[k] = th[k] + scale * ucur[k];
-      if (lane + 64 * k < P) out |= !(y[k] >= lo[k] && y[k] <= hi[k]);
-    }
-    const bool active = (stage == 0 || p.ntry >= 2) && (ahead == 0 || has_next);
-    const bool inb = active && wave_ballot(out) == 0;
-    // the next round's candidates (see load_u)
-    load_u(un1, s + ahead + 1);
-    load_u(un2, s + ahead + 2);
-    dscn = load_sc(s + 1);
-    double r = INFINITY, pr = 0.0;
-    TCI_PHASE(0)
-    if (inb) {
-      double* yb = yl[par][w];
+    for (int q = 0; q < EPW; ++q) {
+      const int h = a1 + 2 * q;  // step s + h
+      double y[NJ];
+      bool out = false;
 #pragma unroll
-      for (int k = 0; k < NJ; ++k) yb[lane + 64 * k] = y[k];
-      wave_sync();
-      e.v = yb[0];
-      e.tau = yb[1];
-      e.ton = yb[2];
-      e.b1 = yb[3];
-      e.b2 = yb[4];
-      e.A = yb[5];
-      e.R = yb[6];
-#pragma unroll
-      for (int q = 0; q < RPL; ++q) {
-        const int g = RPL * lane + q;
-        e.dr[q] = 7 + g < P ? yb[7 + g] : 0.0;
+      for (int k = 0; k < NJ; ++k) {
+        y[k] = th[k] + scale * ucur[q][k];
+        if (lane + 64 * k < P) out |= !(y[k] >= lo[k] && y[k] <= hi[k]);
       }
-      r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
-      TCI_PHASE(1)
-      pr = wave_prior_reg<NJ>(y, mu, sg, P, lane);
-    }
-    if (lane == 0) {
-      xch[par][w][0] = r;
-      xch[par][w][1] = pr;
-      xch[par][w][2] = inb ? 1.0 : 0.0;
+      const bool active = (stage == 0 || p.ntry >= 2) && s + h <= s_end;
+      const bool inb = active && wave_ballot(out) == 0;
+      if (q == 0) {  // the next round's candidates (see load_u)
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) load_u(cand[k], s + a1 + 1 + kPf[k]);
+        dscn = load_sc(s + 1);
+      }
+      double r = INFINITY, pr = 0.0;
+      TCI_PHASE(0)
+      if (inb) {
+        double* yb = yl[par][2 * h + stage];
+#pragma unroll
+        for (int k = 0; k < NJ; ++k) yb[lane + 64 * k] = y[k];
+        wave_sync();
+        e.v = yb[0];
+        e.tau = yb[1];
+        e.ton = yb[2];
+        e.b1 = yb[3];
+        e.b2 = yb[4];
+        e.A = yb[5];
+        e.R = yb[6];
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) {
+          const int g = RPL * lane + k;
+          e.dr[k] = 7 + g < P ? yb[7 + g] : 0.0;
+        }
+        r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
+        TCI_PHASE(1)
+        pr = wave_prior_reg<NJ>(y, mu, sg, P, lane);
+      }
+      if (lane == 0) {
+        xch[par][2 * h + stage][0] = r;
+        xch[par][2 * h + stage][1] = pr;
+        xch[par][2 * h + stage][2] = inb ? 1.0 : 0.0;
+      }
     }
     if (w == kSigWave) {
-      // lanes 0-2: s2 of the last decided row (pending: 1/(Gl*(2/ss))), after step s unmoved
-      // (1/(G_s*(2/ss))), after step s+1 with step s unmoved (1/(G_s+1*(2/ss))); lanes 0-1 also
-      // the precision of that s2, which the decisions of steps s and s+1 use
-      const double Ga = lane_bcast(dsc, sbase + D_G), Gb = lane_bcast(dsc, sbase + 4 + D_G);
-      const double gv = lane == 0 ? Gl : lane == 1 ? Ga : Gb;
+      // lanes 0 .. D-1: s2 of the last decided row (pending: 1/(Gl*(2/ss))), then after the steps
+      // s .. s + i - 1 unmoved (1/(G_{s+i-1}*(2/ss))); their precisions are the decisions' of
+      // steps s .. s + D - 1
+      double gv = Gl;
+#pragma unroll
+      for (int i = 1; i < D; ++i) {
+        const double Gi = lane_bcast(dsc, sbase + 4 * (i - 1) + D_G);
+        gv = lane == i ? Gi : gv;
+      }
       double x = 1.0 / (gv * (2.0 / ss));
       if (!p.updatesigma || (lane == 0 && !gpend)) x = s2c;
       const double ipv = 1.0 / x;
-      if (lane < 2) xip[par][lane] = ipv;
+      if (lane < D) xip[par][lane] = ipv;
       const double x0 = lane_bcast(x, 0);
       flush_s2(x0);
       s2c = x0;
       gpend = false;
-      s2first = lane_bcast(x, 1);  // the s2 of row s if it does not move the chain
+#pragma unroll
+      for (int i = 0; i < D - 1; ++i) s2f[i] = lane_bcast(x, i + 1);  // the s2 of row s + i if unmoved
     }
     if (w == kRecWave) flush_vec();
     if (w == kRecWave) {
@@ -1131,60 +1162,56 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     TCI_PHASE(2)
     __syncthreads();
     TCI_PHASE(3)
-    // ---- decisions: step s, then (if the chain did not move) step s+1 from the speculation.
-    // The three exponentials each step can need -- a12, a32, l2 (dram_log_ratio) -- for both
-    // steps are ONE lane-parallel exp (lanes 0-2: step s, 3-5: step s+1), picked by readlane.
-    const double* X0 = xch[par][0];
-    const double* X1 = xch[par][1];
-    const double* X2 = xch[par][2];
-    const double* X3 = xch[par][3];
-    const bool inb1a = X0[2] != 0.0, inb2a = X1[2] != 0.0, inb1b = X2[2] != 0.0, inb2b = X3[2] != 0.0;
-    const double pr1a = inb1a ? X0[1] : 0.0, pr2a = inb2a ? X1[1] : 0.0;
-    const double pr1b = inb1b ? X2[1] : 0.0, pr2b = inb2b ? X3[1] : 0.0;
-    const int h = lane < 3 ? 0 : 1, k3 = lane < 3 ? lane : lane - 3;  // lanes >= 6 compute junk
-    const double ssA = h ? X2[0] : X0[0], ssB = h ? X3[0] : X1[0];
-    const double prA = h ? pr1b : pr1a, prB = h ? pr2b : pr2a;
-    const double ipu = xip[par][h];
-    // one expression, per-lane operands: a12 (k3 = 0), a32 (k3 = 1), l2 (k3 = 2)
-    const double eA = k3 == 2 ? ssB : ssA, eB = k3 == 1 ? ssB : ss;
-    const double eC = k3 == 2 ? prB : prA, eD = k3 == 1 ? prB : prior;
-    const double ev = exp(dram_log_ratio(eA, eB, eC, eD, ipu));
-    const double av = k3 == 2 ? ev : fmin(1.0, ev);
-    const double a12a = lane_bcast(av, 0), a32a = lane_bcast(av, 1), l2a = lane_bcast(av, 2);
-    const double a12b = lane_bcast(av, 3), a32b = lane_bcast(av, 4), l2b = lane_bcast(av, 5);
+    // ---- decisions: step s, then (while the chain did not move) s + 1, .. s + D - 1 from the
+    // speculation. The three exponentials each step can need -- a12, a32, l2 (dram_log_ratio) --
+    // for every step are ONE lane-parallel exp (lanes 3h .. 3h + 2: step s + h), picked by readlane.
+    const double (*X)[4] = xch[par];
+    double av;
+    {
+      const int h = min(lane / 3, D - 1), k3 = lane - 3 * (lane / 3);  // lanes >= 3D compute junk
+      const double* x1 = X[2 * h];
+      const double* x2 = X[2 * h + 1];
+      const double ssA = x1[0], ssB = x2[0];
+      const double prA = x1[2] != 0.0 ? x1[1] : 0.0, prB = x2[2] != 0.0 ? x2[1] : 0.0;
+      const double ipu = xip[par][h];
+      // one expression, per-lane operands: a12 (k3 = 0), a32 (k3 = 1), l2 (k3 = 2)
+      const double eA = k3 == 2 ? ssB : ssA, eB = k3 == 1 ? ssB : ss;
+      const double eC = k3 == 2 ? prB : prA, eD = k3 == 1 ? prB : prior;
+      const double ev = exp(dram_log_ratio(eA, eB, eC, eD, ipu));
+      av = k3 == 2 ? ev : fmin(1.0, ev);
+    }
     TCI_PHASE(4)
-    const double Q1a = lane_bcast(dsc, sbase + D_Q1), U1a = lane_bcast(dsc, sbase + D_U1);
-    const double U2a = lane_bcast(dsc, sbase + D_U2);
-    const double Q1b = lane_bcast(dsc, sbase + 4 + D_Q1), U1b = lane_bcast(dsc, sbase + 4 + D_U1);
-    const double U2b = lane_bcast(dsc, sbase + 4 + D_U2);
     int adv = 0;
-    for (int hh = 0; hh < 2; ++hh) {
-      if (hh == 1 && !has_next) break;
-      const double* x1 = hh ? X2 : X0;
-      const double* x2 = hh ? X3 : X1;
-      const bool inb1 = hh ? inb1b : inb1a, inb2 = hh ? inb2b : inb2a;
+#pragma unroll
+    for (int hh = 0; hh < D; ++hh) {  // uniform
+      if (hh >= 1 && s + hh > s_end) break;
+      const double* x1 = X[2 * hh];
+      const double* x2 = X[2 * hh + 1];
+      const bool inb1 = x1[2] != 0.0, inb2 = x2[2] != 0.0;
+      const double a12 = lane_bcast(av, 3 * hh), a32 = lane_bcast(av, 3 * hh + 1), l2 = lane_bcast(av, 3 * hh + 2);
+      const double Q1 = lane_bcast(dsc, sbase + 4 * hh + D_Q1), U1 = lane_bcast(dsc, sbase + 4 * hh + D_U1);
+      const double U2 = lane_bcast(dsc, sbase + 4 * hh + D_U2);
       bool acc = false, acc2 = false;
       if (inb1) {
         nev += 1;
-        acc = (hh ? U1b : U1a) < (hh ? a12b : a12a);
+        acc = U1 < a12;
       }
       if (!acc && inb2) {
         nev += 1;
-        acc2 = hh ? dram_dr_accept(U2b, a12b, a32b, l2b, Q1b) : dram_dr_accept(U2a, a12a, a32a, l2a, Q1a);
+        acc2 = dram_dr_accept(U2, a12, a32, l2, Q1);
       }
       const bool moved = acc || acc2;
+      adv = hh + 1;
       if (moved) {
         const double* yb = yl[par][2 * hh + (acc ? 0 : 1)];
 #pragma unroll
         for (int k = 0; k < NJ; ++k) th[k] = yb[lane + 64 * k];
         ss = acc ? x1[0] : x2[0];
-        prior = acc ? (hh ? pr1b : pr1a) : (hh ? pr2b : pr2a);
+        prior = acc ? (inb1 ? x1[1] : 0.0) : (inb2 ? x2[1] : 0.0);
         nacc += 1;
-      } else {
-        nrej += 1;
+        break;  // step s + hh + 1 must be re-proposed around the new state
       }
-      adv = hh + 1;
-      if (moved) break;  // step s+1 must be re-proposed around the new state
+      nrej += 1;
     }
     // the rows s .. s + adv - 1 are recorded next round (s2 of the last: 1/(G*(2/ss)), ss after it)
     prow = s;
@@ -1192,9 +1219,25 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     Gl = lane_bcast(dsc, sbase + 4 * (adv - 1) + D_G);
     gpend = p.updatesigma != 0;
     TCI_PHASE(6)
-    // ---- advance by adv rows: the candidates loaded at the start of this round
+    // ---- advance by adv rows: the candidates loaded at the start of this round (row
+    // s + adv + a1 + 2q is candidate adv + 2q - 1), or a load now
 #pragma unroll
-    for (int k = 0; k < NJ; ++k) ucur[k] = adv == 1 ? un1[k] : un2[k];
+    for (int q = 0; q < EPW; ++q) {
+      bool have = false;
+#pragma unroll
+      for (int i = 0; i < NPF; ++i) have = have || adv + 2 * q - 1 == kPf[i];
+      if (have) {  // uniform
+#pragma unroll
+        for (int k = 0; k < NJ; ++k) {
+          double v = cand[0][k];
+#pragma unroll
+          for (int i = 1; i < NPF; ++i) v = adv + 2 * q - 1 == kPf[i] ? cand[i][k] : v;
+          ucur[q][k] = v;
+        }
+      } else {
+        load_u(ucur[q], s + adv + a1 + 2 * q);
+      }
+    }
     dsc = dscn;
     sbase = 4 * (adv - 1);
     s += adv;
@@ -1435,8 +1478,8 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
     hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, stream, st, p,
                        kp, s_begin, s_end, with_records);
   else
-    hipLaunchKernelGGL((k_chain<RPL, NSEG>), dim3((unsigned)st.n_chains), dim3(kThreads), 0, stream, st, p, kp,
-                       s_begin, s_end, with_records);
+    hipLaunchKernelGGL((k_chain<RPL, NSEG, (RPL <= 2 ? kChainEPW : 1)>), dim3((unsigned)st.n_chains), dim3(kThreads), 0,
+                       stream, st, p, kp, s_begin, s_end, with_records);
   return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;
 }
 
@@ -2182,7 +2225,8 @@ int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& k
   }
 }
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl) {
-  const int64_t chain = (4 * (4 * 64 * rpl + 4 * rpl) + 2 * 4 * 64 * (rpl + 1) + 2 * 4 * 4 + 2 * 2 * 5) * 8;  // k_chain
+  const int64_t ns = 4 * (rpl <= 2 ? kChainEPW : 1);  // k_chain: evl, yl, xch, xip (and slack)
+  const int64_t chain = (4 * (4 * 64 * rpl + 4 * rpl) + 2 * ns * 64 * (rpl + 1) + 2 * ns * 4 + 2 * ns + 16) * 8;
   return std::max<int64_t>(chain, draws_lds_bytes(ld));                                  // k_draws (dynamic)
 }
 int dram_launch_stats(const DramState& st, const DramParams& p, void* stream) {
