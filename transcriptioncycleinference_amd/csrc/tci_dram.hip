@@ -167,17 +167,20 @@ __device__ __forceinline__ bool dram_dr_accept(double u2, double a12, double a32
   return u2 * (1.0 - a12) < l2 * q1 * (1.0 - a32);
 }
 
+// Prior precision of one entry: 1/sig for a finite sig, 0 for sig = +Inf (no prior: the entry adds
+// exactly 0). Every engine forms ((th - mu) * (1/sig))^2 from it -- one rounding more than MATLAB's
+// ((th - mu)./sig).^2 per entry, the same bits in every engine; the chain kernels take the
+// reciprocal once per chunk instead of dividing at every evaluation.
+__device__ __forceinline__ double prior_prec(double sg) { return isfinite(sg) ? 1.0 / sg : 0.0; }
+
 // Prior SS sum(((th - mu)./sig).^2) over finite sig (mcmcstat's default priorfun) by ONE wave:
 // lane l sums j = l, l + 64, .. in order, then a fixed xor-shuffle tree. Both engines call this,
 // so the bits agree.
 __device__ double wave_prior(const double* th, const double* mu, const double* sig, int P, int lane) {
   double s = 0.0;
   for (int j = lane; j < P; j += 64) {
-    const double sg = sig[j];
-    if (isfinite(sg)) {
-      const double z = (th[j] - mu[j]) / sg;
-      s += z * z;
-    }
+    const double z = (th[j] - mu[j]) * prior_prec(sig[j]);
+    s += z * z;
   }
   return wsum64(s);
 }
@@ -209,11 +212,8 @@ __device__ double block_sum(double x, double* red) {
 __device__ double prior_ss(const double* th, const double* mu, const double* sig, int P, double* red) {
   double s = 0.0;
   for (int j = threadIdx.x; j < P; j += kThreads) {
-    const double sg = sig[j];
-    if (isfinite(sg)) {
-      const double z = (th[j] - mu[j]) / sg;
-      s += z * z;
-    }
+    const double z = (th[j] - mu[j]) * prior_prec(sig[j]);
+    s += z * z;
   }
   return block_sum(s, red);
 }
@@ -720,15 +720,15 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
   }
 }
 
-// wave_prior on register-held vectors (entry k of lane l is j = l + 64 k): the same per-lane
-// order and shuffle tree, so the same bits.
+// wave_prior on register-held vectors (entry k of lane l is j = l + 64 k; rs[k] = prior_prec of
+// its sig): the same per-lane order and shuffle tree, so the same bits.
 template <int NJ>
-__device__ __forceinline__ double wave_prior_reg(const double* y, const double* mu, const double* sg, int P, int lane) {
+__device__ __forceinline__ double wave_prior_reg(const double* y, const double* mu, const double* rs, int P, int lane) {
   double s = 0.0;
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
-    if (lane + 64 * k < P && isfinite(sg[k])) {
-      const double z = (y[k] - mu[k]) / sg[k];
+    if (lane + 64 * k < P) {
+      const double z = (y[k] - mu[k]) * rs[k];
       s += z * z;
     }
   }
@@ -988,7 +988,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     lo[k] = in ? st.lower[c * ld + j] : 0.0;
     hi[k] = in ? st.upper[c * ld + j] : 0.0;
     mu[k] = in ? st.pmu[c * ld + j] : 0.0;
-    sg[k] = in ? st.psig[c * ld + j] : 0.0;
+    sg[k] = in ? prior_prec(st.psig[c * ld + j]) : 0.0;  // the precision (prior_prec)
   }
   EvalIn<RPL> e;  // the chain's cell records stay in registers
   {
@@ -1337,7 +1337,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
       lo[k] = in ? st.lower[c * ld + j] : 0.0;
       hi[k] = in ? st.upper[c * ld + j] : 0.0;
       mu[k] = in ? st.pmu[c * ld + j] : 0.0;
-      sg[k] = in ? st.psig[c * ld + j] : 0.0;
+      sg[k] = in ? prior_prec(st.psig[c * ld + j]) : 0.0;  // the precision (prior_prec)
     }
   }
   EvalIn<RPL> e;  // the chain's cell records stay in registers
@@ -1362,7 +1362,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         lo[k] = in ? st.lower[c * ld + j] : 0.0;
         hi[k] = in ? st.upper[c * ld + j] : 0.0;
         mu[k] = in ? st.pmu[c * ld + j] : 0.0;
-        sg[k] = in ? st.psig[c * ld + j] : 0.0;
+        sg[k] = in ? prior_prec(st.psig[c * ld + j]) : 0.0;  // the precision (prior_prec)
       }
     }
 #pragma unroll
