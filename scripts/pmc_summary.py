@@ -4,7 +4,9 @@
 HBM traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 bytes, following
 MI355X_MICROARCH.md's HBM/rocprofv3 section: FETCH_SIZE (KB) reads 1/2 of the bytes of a wide
 coalesced read on gfx950; WRITE_SIZE is exact for streaming stores. The x2 read correction is
-calibrated for 16-B-per-lane reads; this kernel's theta reads are 8-16 B per lane (noted).
+measured for this kernel's own load shapes: scripts/calib/fetch_calib.py reads 64 and 256 MB once
+with 8-B and with 16-B per-lane loads, and FETCH_SIZE is half the bytes read in every case
+(profiles/r03_calib/fetch_size_calibration.json).
 Usage: python scripts/pmc_summary.py gpurun_out/<tag> <workload> > profiles/pmc_traffic.json
 """
 import collections
@@ -31,8 +33,8 @@ def main(prefix, workload):
         "hbm_bytes_per_launch": None if fetch is None or write is None else (2 * fetch + write) * 1024,
         "fetch_size_kb_raw": fetch,
         "write_size_kb": write,
-        "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE reads 1/2 of wide streaming reads; "
-                      "calibrated for 16-B/lane reads, theta rows here are read 8-16 B/lane)",
+        "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts exactly 1/2 of the bytes read "
+                      "with 8-B and 16-B per-lane loads: profiles/r03_calib/fetch_size_calibration.json)",
         "counters_mean_per_launch": mean,
     }
     print(json.dumps(out, indent=1))
