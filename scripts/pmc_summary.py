@@ -11,6 +11,7 @@ Usage: python scripts/pmc_summary.py gpurun_out/<tag> <workload> > profiles/pmc_
 """
 import collections
 import csv
+import glob
 import json
 import sys
 
@@ -18,10 +19,8 @@ import sys
 def main(prefix, workload):
     agg = collections.defaultdict(list)
     for p in range(1, 7):
-        try:
-            rows = list(csv.DictReader(open(f"{prefix}_p{p}/pmc_counter_collection.csv")))
-        except OSError:
-            continue
+        files = glob.glob(f"{prefix}_p{p}/**/*counter_collection.csv", recursive=True)
+        rows = [r for f in files for r in csv.DictReader(open(f))]
         for r in rows:
             if "tci_cohort_kernel" in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
