@@ -841,8 +841,28 @@ struct S2Acc {
   }
 };
 
-// The records of the window ending at row `last` from its logs, by one wave (k_walk at a window's
-// end, k_stats): the rows in row order, kStatsRows loads in flight per column block.
+// The s2 records of the window ending at row `last` from its log, by one wave: 64 rows per pass in
+// lanes, added in row order through lane broadcasts (S2Acc::add, as k_chain adds them);
+// with_out: also the thinned s2 rows.
+__device__ void window_s2_records(const DramState& st, const DramParams& p, int64_t c, int64_t last, int lane,
+                                  bool with_out) {
+  const int64_t first = win_first(p, last);
+  const int nrow = (int)(last - first + 1);
+  const double* lg = st.s2log + c * p.win;
+  S2Acc q{0.0, 0.0, 0.0, first > 1 ? st.sq_mean[c] : sqrt(lg[0])};
+  for (int r0 = 0; r0 < nrow; r0 += 64) {
+    const int r = r0 + lane;
+    const double v = lg[min(r, nrow - 1)];
+    int64_t k;
+    if (with_out && st.s2_out != nullptr && r < nrow && kept_row(p, first + r, k)) st.s2_out[k * st.n_chains + c] = v;
+    const int m = min(64, nrow - r0);
+    for (int l = 0; l < m; ++l) q.add(lane_bcast(v, l));
+  }
+  if (lane == 0) q.finish(st, c, first, last);
+}
+
+// The records of the window ending at row `last` from its logs, by one wave (k_stats): the rows in
+// row order, kStatsRows loads in flight per column block.
 constexpr int kStatsRows = 32;
 __device__ void window_records(const DramState& st, const DramParams& p, int64_t c, int64_t last, int lane) {
   const int64_t ld = st.ld;
@@ -872,18 +892,7 @@ __device__ void window_records(const DramState& st, const DramParams& p, int64_t
     }
     a.finish(st, p, c, last, P, j);
   }
-  // s2: 64 rows per pass in lanes, added in row order through lane broadcasts
-  const double* lg = st.s2log + c * p.win;
-  S2Acc q{0.0, 0.0, 0.0, first > 1 ? st.sq_mean[c] : sqrt(lg[0])};
-  for (int r0 = 0; r0 < nrow; r0 += 64) {
-    const int r = r0 + lane;
-    const double v = lg[min(r, nrow - 1)];
-    int64_t k;
-    if (st.s2_out != nullptr && r < nrow && kept_row(p, first + r, k)) st.s2_out[k * st.n_chains + c] = v;
-    const int m = min(64, nrow - r0);
-    for (int l = 0; l < m; ++l) q.add(lane_bcast(v, l));
-  }
-  if (lane == 0) q.finish(st, c, first, last);
+  window_s2_records(st, p, c, last, lane, true);
 }
 
 // The batched engine's records (and a run's first or last window outside a chunk): one wave per
@@ -1314,6 +1323,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   constexpr int NW = kThreads / 64;
   __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each wave's {K,J} tables / rows
   __shared__ double yl[NW][64 * NJ];                            // each wave's proposal (theta broadcast)
+  __shared__ double racc[NW][3][64 * NJ];  // each wave's window column sums ws, S1, S2 (ColAcc, in LDS)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int lane = threadIdx.x & 63;  // re-laundered every step (launder_lane)
   const int64_t c = (int64_t)blockIdx.x * NW + w;
@@ -1349,6 +1359,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   int64_t nev = st.nevals[c];
   double* yb = yl[w];
   const int64_t slot0 = log_slot(p, s_begin) - s_begin;  // log slot of row s: slot0 + s
+  // the window's column sums as the rows are decided, k_chain's ColAcc arithmetic ("Chain
+  // records"): the sums in this wave's LDS (registers are at the 2-waves/SIMD budget), their shift K
+  // in registers, continuing a window begun by an earlier chunk (or by k_init_stats); the s2 sums
+  // from the window's s2 log at its end (S2Acc over 100 values)
+  ColAcc<NJ> ca;  // only first / sf / kfirst / K live in the loop
+  ca.setup(p, s_begin);
+  const bool cont = s_begin != ca.first;
+  double* ra = racc[w][0];
+  double* rb = racc[w][1];
+  double* rc = racc[w][2];
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    const int j = lane + 64 * k;
+    const bool in = j < P;
+    ra[64 * k + lane] = cont && in ? st.wsumv[c * ld + j] : 0.0;
+    rb[64 * k + lane] = cont && in ? st.wacc1[c * ld + j] : 0.0;
+    rc[64 * k + lane] = cont && in ? st.wacc2[c * ld + j] : 0.0;
+    ca.K[k] = !in ? 0.0 : !ca.kfirst ? st.smean[c * ld + j] : cont ? st.window[c * p.win * ld + j] : 0.0;
+  }
   // ssfun and prior of the proposal th + scale * u (k_chain's per-wave evaluation); an in-bounds
   // proposal is left in yb (a move copies it from there)
   auto evaluate = [&](const double* u, double scale, double& r, double& pr) {
@@ -1437,8 +1466,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     // sigma2 Gibbs update of this row (updatesigma = 1, :265): 1/sigma2 ~ Gamma(N/2, scale 2/ss)
     if (p.updatesigma) s2 = 1.0 / (G * (2.0 / ss));
     wave_sync();  // yb reads are done before the next evaluation rewrites it
-    log_row<NJ>(st, p, c, slot0 + s, P, th, lane);  // the row's records: k_stats, after the chunk
+    log_row<NJ>(st, p, c, slot0 + s, P, th, lane);
     if (lane == 0) log_s2(st, p, c, slot0 + s, s2);
+    {  // ColAcc::add of row s, the sums in LDS
+      int64_t kk;
+      const bool keep = st.chain_out != nullptr && kept_row(p, s, kk);
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) {
+        if (ca.kfirst && s == ca.first) ca.K[k] = th[k];
+        const int i = 64 * k + lane;
+        ra[i] = ra[i] + th[k];
+        if (s >= ca.sf) {
+          const double d = th[k] - ca.K[k];
+          rb[i] = rb[i] + d;
+          rc[i] = fma(d, d, rc[i]);
+        }
+        if (keep && lane + 64 * k < P) st.chain_out[(kk * st.n_chains + c) * ld + lane + 64 * k] = th[k];
+      }
+      if (st.s2_out != nullptr && lane == 0 && kept_row(p, s, kk)) st.s2_out[kk * st.n_chains + c] = s2;
+    }
   }
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
@@ -1454,9 +1500,26 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     st.nevals[c] = nev;
     if (c == 0) *st.step = s_end;  // the adaptation reads the row it follows
   }
-  if (with_records) {  // the chunk ends a window (or the run): its records, from the logs just written
+  if (with_records) {  // the chunk ends a window (or the run): its records
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      ca.ws[k] = ra[64 * k + lane];
+      ca.S1[k] = rb[64 * k + lane];
+      ca.S2[k] = rc[64 * k + lane];
+    }
+    ca.finish(st, p, c, s_end, P, lane);
     __threadfence_block();  // lane 0's s2 logs before the other lanes read them
-    window_records(st, p, c, s_end, lane);
+    window_s2_records(st, p, c, s_end, lane, false);  // the s2 sums from the window's log (100 values)
+  } else {  // the window goes on in the next chunk
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      const int j = lane + 64 * k;
+      if (j < P) {
+        st.wsumv[c * ld + j] = ra[64 * k + lane];
+        st.wacc1[c * ld + j] = rb[64 * k + lane];
+        st.wacc2[c * ld + j] = rc[64 * k + lane];
+      }
+    }
   }
 }
 
