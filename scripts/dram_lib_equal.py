@@ -29,7 +29,7 @@ def run(lib, steps, n, cfg):
     for k, r in enumerate(fr.MCMCresults):
         sc = [r[f] for f in sorted(r) if np.isscalar(r[f]) and isinstance(r[f], float)]
         rows.append(np.concatenate([sc, r["mean_dR"], r["sigma_dR"], fr.final_theta[k], [fr.accept_rate[k]]]))
-    return np.array(rows + [np.full(len(rows[0]), float(fr.n_evals))])
+    return np.concatenate(rows + [np.atleast_1d(np.asarray(fr.n_evals, np.float64)).ravel()])  # ragged rows: flat
 
 
 a, b = sys.argv[1], sys.argv[2]

@@ -1587,31 +1587,60 @@ __device__ __forceinline__ double row_to_all(double x) {
   return __hiloint2double((int)h[1], (int)h[0]);
 }
 
-// Step K of the Cholesky factorization A = U'U of a symmetric 16 x 16 tile held by ONE wave in
-// registers, in the MFMA accumulator layout (lane 16 g + j holds rows g, g+4, g+8, g+12 of
-// column j). Rows and columns > K take the symmetric rank-1 update A -= a_K a_K' / d (both
-// triangles, so column K is a row broadcast: A[i][K] = A[K][i]); row K keeps A[K][j] and its pivot
-// d goes to dpiv[K]. The dependent chain per step is a readlane, a reciprocal (v_rcp_f64 and one
-// Newton step) and one FMA; the square roots are left to chol16_finish.
+// Steps K and K+1 (K even) of the Cholesky factorization A = U'U of a symmetric 16 x 16 tile held
+// by ONE wave in registers, in the MFMA accumulator layout (lane 16 g + j holds rows g, g+4, g+8,
+// g+12 of column j). Pivot by pivot, rows and columns > K take the symmetric rank-1 update
+// A -= a_K a_K' / d (both triangles, so column K is a row broadcast); row K keeps A[K][j] and its
+// pivot d goes to dpiv[K]; the square roots are left to chol16_finish. Two pivots per call: the
+// pivot-block entries are read together and every element takes both rank-1 updates back to back,
+// with the operands the one-pivot recurrence forms -- the column-(K+1) values after step K,
+// A'[i][K+1] = fma(-A[i][K], A[K][K+1]*rd0, A[i][K+1]), row K+1 after step K,
+// A'[K+1][j] = fma(-A[K+1][K], A[K][j]*rd0, A[K+1][j]), and the pivot d1' from it -- so the bits
+// are the one-pivot form's (bitwise-equal fits, r03ag). Half the pivot round trips (readlane ->
+// v_rcp_f64 + Newton -> update -> readlane) of the one wave that factors the tile, ~25 % fewer
+// instructions: k_adapt_mfma 112.2 -> 109.3 us per TestData adaptation (r03af).
 template <int K>
-__device__ __forceinline__ void chol16_step(double (&a)[4], int lane, double* dpiv, bool& bad) {
+__device__ __forceinline__ void chol16_step2(double (&a)[4], int lane, double* dpiv, bool& bad) {
   if constexpr (K < 16) {
-    constexpr int kg = K & 3, kr = K >> 2;
+    constexpr int kg0 = K & 3, kr0 = K >> 2, kg1 = (K + 1) & 3, kr1 = (K + 1) >> 2;
     const int g = lane >> 4, j = lane & 15;
-    const double d = lane_bcast(a[kr], 16 * kg + K);
-    bad = bad || !(d > 0.0) || !isfinite(d);
-    double rd = __builtin_amdgcn_rcp(d);
-    rd = fma(rd, fma(-d, rd, 1.0), rd);
-    const double akj = row_to_all<kg>(a[kr]);  // A[K][j]
-    double aik[4];
+    const double d0 = lane_bcast(a[kr0], 16 * kg0 + K);      // A[K][K]
+    const double b = lane_bcast(a[kr0], 16 * kg0 + K + 1);   // A[K][K+1]
+    const double bl = lane_bcast(a[kr1], 16 * kg1 + K);      // A[K+1][K] (the updates leave the two
+                                                              // triangles equal only up to rounding)
+    const double d1 = lane_bcast(a[kr1], 16 * kg1 + K + 1);  // A[K+1][K+1]
+    const double akj0 = row_to_all<kg0>(a[kr0]);              // A[K][j]
+    const double akj1 = row_to_all<kg1>(a[kr1]);              // A[K+1][j]
+    double aik0[4], aik1[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) aik[q] = row_bcast16<K>(a[q]);  // A[g + 4q][K]
-    const double sj = akj * rd;
+    for (int q = 0; q < 4; ++q) {
+      aik0[q] = row_bcast16<K>(a[q]);      // A[g + 4q][K]
+      aik1[q] = row_bcast16<K + 1>(a[q]);  // A[g + 4q][K+1]
+    }
+    double rd0 = __builtin_amdgcn_rcp(d0);
+    rd0 = fma(rd0, fma(-d0, rd0, 1.0), rd0);
+    const double sj0 = akj0 * rd0;
+    const double s01 = b * rd0;                    // sj0 of column K+1
+    const double d1p = fma(-bl, s01, d1);          // A'[K+1][K+1]
+    double rd1 = __builtin_amdgcn_rcp(d1p);
+    rd1 = fma(rd1, fma(-d1p, rd1, 1.0), rd1);
+    const double akj1p = j > K ? fma(-bl, sj0, akj1) : akj1;  // A'[K+1][j] (row K+1 after step K)
+    const double sj1 = akj1p * rd1;
+    bad = bad || !(d0 > 0.0) || !isfinite(d0) || !(d1p > 0.0) || !isfinite(d1p);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (g + 4 * q > K && j > K) a[q] = fma(-aik[q], sj, a[q]);
-    if (lane == 0) dpiv[K] = d;
-    chol16_step<K + 1>(a, lane, dpiv, bad);
+    for (int q = 0; q < 4; ++q) {
+      const int i = g + 4 * q;
+      const double aik1p = fma(-aik0[q], s01, aik1[q]);  // A'[i][K+1]
+      double t = a[q];
+      if (i > K && j > K) t = fma(-aik0[q], sj0, t);
+      if (i > K + 1 && j > K + 1) t = fma(-aik1p, sj1, t);
+      a[q] = t;
+    }
+    if (lane == 0) {
+      dpiv[K] = d0;
+      dpiv[K + 1] = d1p;
+    }
+    chol16_step2<K + 2>(a, lane, dpiv, bad);
   }
 }
 
@@ -1641,14 +1670,14 @@ __device__ __forceinline__ void chol16_finish(double (&a)[4], int lane, double* 
 //     v_mfma_f64_16x16x4_f64 products into the owned tiles, merged with (cov, mean, wsum) by the
 //     pairwise-update formula (mcmcstat's row-by-row recurrence in exact arithmetic);
 //   Cholesky cov + qcovadj I = U'U, right-looking by 16-column panels: the owners copy panel row pk
-//     to LDS (the diagonal tile factored on the way, in its owner's registers: chol16_step),
+//     to LDS (the diagonal tile factored on the way, in its owner's registers: chol16_step2),
 //     16-lane groups solve the panel's row tiles (one column per lane), the owners take their U
 //     tiles back and every trailing tile takes the rank-16 update as 4 MFMAs on its owner's
 //     registers. R = U * adascale, stored only when the
 //     whole factorization succeeded (a singular matrix keeps the previous R, as mcmcstat).
 // Instances: NW waves per workgroup (one chain), MAXT = max tiles per dimension, kAdOwn output tiles
-// per wave (MAXT (MAXT + 1) / 2 <= NW kAdOwn): <4, 9> for P <= 144 (two chains per CU), <8, 13>
-// for P <= 208 (configs 4/5: 200 points, P = 207; one chain per CU at 256 VGPRs per wave).
+// per wave (MAXT (MAXT + 1) / 2 <= NW kAdOwn): <8, 9, 6> for P <= 144 (two chains per CU at 128
+// VGPRs), <8, 13, 12> for P <= 208 (configs 4/5: 200 points, P = 207; one chain per CU).
 constexpr int kAdRB = 16;   // window rows per LDS batch
 __host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P) {
   const int64_t NT = (P + 15) / 16, LX = 16 * NT;
@@ -1656,13 +1685,17 @@ __host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P) {
   return (shared + 2 * LX) * 8;
 }
 
-template <int NW, int MAXT, int kAdOwn>  // kAdOwn: output tiles per wave (a multiple of the merge group)
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8 ? 2 : NW / 4))) void k_adapt_mfma(
+template <int NW, int MAXT, int kAdOwn, int WPE = (NW <= 8 ? 2 : NW / 4)>  // kAdOwn: output tiles per wave (a
+                                                                        // multiple of the merge group); WPE: waves/SIMD
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_adapt_mfma(
     DramState st, DramParams p) {
   constexpr int kAdM = MAXT;
   constexpr int NTH = 64 * NW;
   static_assert(MAXT * (MAXT + 1) / 2 <= NW * kAdOwn, "owned tiles per wave");
-  static_assert(kAdOwn % 6 == 0, "owned tiles come in merge groups of 6");
+  // merge groups: every old value of a group's tiles is read before any of them is written (a
+  // diagonal tile reads the mirrors of its own elements; tiles never share an element)
+  constexpr int kAdMG = kAdOwn <= 6 ? 3 : 6;
+  static_assert(kAdOwn % kAdMG == 0, "owned tiles come in whole merge groups");
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int fail;
   __shared__ double rdg[16];  // 1 / U[k][k] of the current diagonal tile
@@ -1754,7 +1787,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8
   // in groups of kAdMG tiles: a group's old values are all read before any of them is written (a
   // diagonal tile reads the mirrors of its own elements)
   const double rn1 = 1.0 / (nn - 1.0);
-  constexpr int kAdMG = 6;
 #pragma unroll
   for (int o0 = 0; o0 < kAdOwn; o0 += kAdMG) {
     if (o0 >= nown) break;  // uniform
@@ -1836,7 +1868,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8
     }
     if (own_diag) {  // uniform
       bool bad = false;
-      chol16_step<0>(dt, lane, rdg, bad);
+      chol16_step2<0>(dt, lane, rdg, bad);
       wave_sync();
       chol16_finish(dt, lane, rdg, rdg);
 #pragma unroll
@@ -1916,7 +1948,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW <= 8
 //     LDS in batches of rb rows (as many as fit 96 KB, a multiple of 4) and accumulates the owned
 //     tiles' scatter with v_mfma_f64_16x16x4_f64, then merges them into (cov, mean, wsum) with
 //     k_adapt_mfma's formula and writes cov + qcovadj I to the tile grid;
-//   Cholesky: per panel pk, wave 0 factors the diagonal tile in registers (chol16_step), 16-lane
+//   Cholesky: per panel pk, wave 0 factors the diagonal tile in registers (chol16_step2), 16-lane
 //     groups solve the panel's row tiles, every wave takes trailing tiles (pk < ti <= tj) round-robin
 //     and applies the rank-16 update as 4 MFMAs. R = U * adascale, stored only when every pivot
 //     was positive (a singular matrix keeps the previous R, as mcmcstat).
@@ -2093,7 +2125,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
       for (int q = 0; q < 4; ++q) dt[q] = A[(kq + 4 * q) * 16 + row];
       bool bad = false;
-      chol16_step<0>(dt, lane, rdg, bad);
+      chol16_step2<0>(dt, lane, rdg, bad);
       wave_sync();
       chol16_finish(dt, lane, rdg, rdg);
 #pragma unroll
@@ -2239,10 +2271,10 @@ int launch_stage(void (*k)(DramState, DramParams), const DramState& st, const Dr
   return finish();
 }
 
-template <int NW, int MAXT, int OWN>
+template <int NW, int MAXT, int OWN, int WPE = (NW <= 8 ? 2 : NW / 4)>
 int launch_adapt_mfma(const DramState& st, const DramParams& p, void* stream) {
   const size_t bytes = (size_t)adapt_mfma_lds_bytes(p.pmax);
-  auto k = k_adapt_mfma<NW, MAXT, OWN>;
+  auto k = k_adapt_mfma<NW, MAXT, OWN, WPE>;
   if (ensure_dyn_lds((const void*)k, bytes) != TCI_OK) return TCI_EHIP;
   hipLaunchKernelGGL(k, chain_grid(st.n_chains), dim3(64 * NW), bytes, (hipStream_t)stream, st, p);
   return finish();
@@ -2268,7 +2300,9 @@ int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream) 
   return launch_stage(k_accept2, st, p, stream);
 }
 int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
-  if (p.pmax <= 16 * 9) return launch_adapt_mfma<4, 9, 12>(st, p, stream);
+  // P <= 144: 8 waves x 6 tiles at <= 128 VGPRs (two chains per CU): 109.3 -> 105.2 us per
+  // TestData adaptation against 4 waves x 12 tiles (r03af; 28 VGPRs spilled, still faster)
+  if (p.pmax <= 16 * 9) return launch_adapt_mfma<8, 9, 6, 4>(st, p, stream);
   // P <= 208: 8 waves x 12 tiles (16 waves x 6 tiles measured slower)
   if (p.pmax <= 16 * 13) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
   const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax);
