@@ -565,3 +565,31 @@ def test_very_long_cells_sample_and_adapt(n):
         assert np.all(np.tril(R, -1) == 0)
         want = (2.4 ** 2 / P) * C
         np.testing.assert_allclose(R.T @ R, want, rtol=1e-10, atol=1e-10 * np.abs(want).max())  # FP64 R, P <= 520
+
+
+def test_walk_at_10000_chains_equals_fused_and_batched():
+    """BASELINE config 4 at its full chain count (10,000 synthetic cells x 200 points, one chain per
+    cell): WALK -- what AUTO runs there -- against FUSED and the batched engine, bit for bit, over
+    two adaptation windows (chunks cut by the draws-buffer cap, windows continuing across chunks);
+    every output finite."""
+    import bench
+    from transcriptioncycleinference_amd import Likelihood
+    from transcriptioncycleinference_amd.mcmc import DramOptions, fit
+
+    cells, _, construct = bench.synthetic_config_cells(4, 0, 1, 0)[:3]
+    assert cells.n_cells == 10000
+    out = {}
+    with Likelihood(cells, construct, device=0) as L:
+        for eng in ("walk", "fused", "batched"):
+            fr = fit(L, n_steps=240, n_burn=120, seed=5, opts=DramOptions(engine=eng))
+            out[eng] = fr
+    w = out["walk"]
+    assert np.all(np.isfinite(w.final_theta)) and np.all(np.isfinite([r["mean_v"] for r in w.MCMCresults]))
+    assert np.median(w.accept_rate) > 0.01
+    for eng in ("fused", "batched"):
+        o = out[eng]
+        np.testing.assert_array_equal(o.final_theta, w.final_theta, err_msg=eng)
+        np.testing.assert_array_equal(o.accept_rate, w.accept_rate, err_msg=eng)
+        np.testing.assert_array_equal(o.n_evals, w.n_evals, err_msg=eng)
+        np.testing.assert_array_equal([r["mean_v"] for r in o.MCMCresults], [r["mean_v"] for r in w.MCMCresults],
+                                      err_msg=eng)
