@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Bitwise comparison of two library builds on the same DRAM fit (A/B of a change that must not
 move any bit): python scripts/dram_lib_equal.py LIB_A LIB_B [STEPS] [CELLS] [CFG]
-("main" = the in-tree build). CFG 0: TestData cells; 4/5: BASELINE config-4/5 synthetic cells
+("main" = the in-tree build; "LIB@NAME=VALUE" also sets the environment variable NAME for that
+run, e.g. main@TCI_DRAM_OVERLAP=0 against main). CFG 0: TestData cells; 4/5: BASELINE config-4/5 synthetic cells
 (TCI_SYNTH_POINTS points per cell, default 200)."""
 import json
 import os
@@ -15,6 +16,10 @@ from transcriptioncycleinference_amd.mcmc import DramOptions, fit  # noqa: E402
 
 
 def run(lib, steps, n, cfg):
+    lib, _, env = lib.partition("@")
+    if env:
+        k, _, v = env.partition("=")
+        os.environ[k] = v
     path = None if lib == "main" else lib
     if cfg == 0:
         cells, con = testdata(), "P2P-MS2v5-LacZ-PP7v4"
@@ -24,6 +29,8 @@ def run(lib, steps, n, cfg):
     engine = os.environ.get("TCI_ENGINE", "auto")
     with Likelihood(cells, con, lib_path=path) as lk:
         fr = fit(lk, n_steps=steps, n_burn=steps // 4, seed=3, cells=list(range(n)), opts=DramOptions(engine=engine))
+    if env:
+        os.environ.pop(k)
     # every output: the scalar summaries, mean/sigma of dR, the final states, acceptance, evaluations
     rows = []
     for k, r in enumerate(fr.MCMCresults):
