@@ -360,7 +360,8 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t szM = al((size_t)C * sizeof(CellMeta)), szS = al(total * sizeof(tci::StepRec)),
                szP = al(total * sizeof(tci::PointRec));
-  const size_t bytes = szM + 2 * szS + szP;
+  const size_t szT = al(64 * sizeof(double));
+  const size_t bytes = szM + 2 * szS + szP + szT;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) return bail(hip_fail(ctx, e, "hipSetDevice"));
   e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
@@ -380,7 +381,15 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
   kp.steps = (const tci::StepRec*)put(steps.data(), total * sizeof(tci::StepRec), szS);
   kp.steps_raw = (const tci::StepRec*)put(steps_raw.data(), total * sizeof(tci::StepRec), szS);
   kp.points = (const tci::PointRec*)put(points.data(), total * sizeof(tci::PointRec), szP);
-  if (!kp.cells || !kp.steps || !kp.steps_raw || !kp.points)
+  double thr[64] = {0.0};
+  for (int k = 0; k < construct->n_seg; ++k) {
+    thr[1 + 4 * k] = construct->ms2_start[k];
+    thr[2 + 4 * k] = construct->ms2_end[k];
+    thr[3 + 4 * k] = construct->pp7_start[k];
+    thr[4 + 4 * k] = construct->pp7_end[k];
+  }
+  kp.thr = (const double*)put(thr, sizeof(thr), szT);
+  if (!kp.cells || !kp.steps || !kp.steps_raw || !kp.points || !kp.thr)
     return bail(fail(ctx, TCI_EHIP, "hipMemcpy(cell table) failed"));
   kp.cell_stride = stride;
   kp.max_n = ctx->max_points;

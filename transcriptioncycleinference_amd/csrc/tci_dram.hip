@@ -723,7 +723,7 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
 // wave_prior on register-held vectors (entry k of lane l is j = l + 64 k; rs[k] = prior_prec of
 // its sig): the same per-lane order and shuffle tree, so the same bits.
 template <int NJ>
-__device__ __forceinline__ double wave_prior_reg(const double* y, const double* mu, const double* rs, int P, int lane) {
+__device__ __forceinline__ double prior_part(const double* y, const double* mu, const double* rs, int P, int lane) {
   double s = 0.0;
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
@@ -732,7 +732,11 @@ __device__ __forceinline__ double wave_prior_reg(const double* y, const double* 
       s += z * z;
     }
   }
-  return wsum64(s);
+  return s;
+}
+template <int NJ>
+__device__ __forceinline__ double wave_prior_reg(const double* y, const double* mu, const double* rs, int P, int lane) {
+  return wsum64(prior_part<NJ>(y, mu, rs, P, lane));
 }
 
 // The fused engines' per-row logs (k_chain / k_walk: one wave writes a row).
@@ -1132,9 +1136,15 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
           const int g = RPL * lane + k;
           e.dr[k] = 7 + g < P ? yb[7 + g] : 0.0;
         }
-        r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
-        TCI_PHASE(1)
-        pr = wave_prior_reg<NJ>(y, mu, sg, P, lane);
+        if (RPL <= 2) {  // the prior's wave sum rides on the evaluation's final scan (same bits)
+          pr = prior_part<NJ>(y, mu, sg, P, lane);
+          r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0, &pr);
+          TCI_PHASE(1)
+        } else {
+          r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
+          TCI_PHASE(1)
+          pr = wave_prior_reg<NJ>(y, mu, sg, P, lane);
+        }
       }
       if (lane == 0) {
         xch[par][2 * h + stage][0] = r;

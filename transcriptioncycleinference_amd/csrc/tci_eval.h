@@ -83,6 +83,23 @@ __device__ __forceinline__ double wave_incl_scan(double x) {
   return x;
 }
 
+// Two independent scans stage by stage (each value's adds in wave_incl_scan's order, so the same
+// bits): the second one's DPP moves fill the first one's wait states.
+__device__ __forceinline__ void wave_incl_scan2(double& x, double& y) {
+  x = x + dpp_f64<0x111, 0xF>(x);
+  y = y + dpp_f64<0x111, 0xF>(y);
+  x = x + dpp_f64<0x112, 0xF>(x);
+  y = y + dpp_f64<0x112, 0xF>(y);
+  x = x + dpp_f64<0x114, 0xF>(x);
+  y = y + dpp_f64<0x114, 0xF>(y);
+  x = x + dpp_f64<0x118, 0xF>(x);
+  y = y + dpp_f64<0x118, 0xF>(y);
+  x = x + dpp_f64<0x142, 0xA>(x);
+  y = y + dpp_f64<0x142, 0xA>(y);
+  x = x + dpp_f64<0x143, 0xC>(x);
+  y = y + dpp_f64<0x143, 0xC>(y);
+}
+
 __device__ __forceinline__ double lane63(double x) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(x), 63);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(x), 63);
@@ -171,17 +188,12 @@ struct Cuts {
 
 // Lane j holds threshold j: 0 -> L, 1 + 4k .. 4 + 4k -> MS2 a, MS2 e, PP7 a, PP7 e of segment k.
 // Returns false (take the exact sweep) when any cut is flagged.
+// xt: this lane's construct threshold from the context's table (KParams::thr, loaded by the caller
+// ahead of time; one load instead of 4 NSEG lane selects); lane 0 takes L, which depends on theta.
 template <int NSEG>
-__device__ __forceinline__ bool distance_cuts(const SegParams* sm, const SegParams* sp, double L, double vd0,
-                                              double eps, int nsteps, int lane, Cuts<NSEG>& cu) {
-  double x = L;
-#pragma unroll
-  for (int k = 0; k < NSEG; ++k) {
-    x = lane == 1 + 4 * k ? sm[k].a : x;
-    x = lane == 2 + 4 * k ? sm[k].e : x;
-    x = lane == 3 + 4 * k ? sp[k].a : x;
-    x = lane == 4 + 4 * k ? sp[k].e : x;
-  }
+__device__ __forceinline__ bool distance_cuts(double xt, double L, double vd0, double eps, int nsteps, int lane,
+                                              Cuts<NSEG>& cu) {
+  const double x = lane == 0 ? L : xt;
   bool bad;
   const int cnt = distance_cut(x, vd0, __builtin_amdgcn_rcp(vd0), eps, nsteps, bad);
   constexpr uint64_t used = (1ull << (1 + 4 * NSEG)) - 1;
@@ -274,11 +286,13 @@ __device__ __forceinline__ void load_cell(const KParams& kp, int c, int lane, Ev
 
 // One ssfun evaluation (MODE_SS: returns the SS, wave-uniform) or forward model (rows written
 // to out0/out1 row b) by one wavefront, on its LDS (2 * (2*64*RPL + 2*RPL) doubles). Needs
-// 2 <= N = e.cm.n <= 64*RPL + 1.
+// 2 <= N = e.cm.n <= 64*RPL + 1. aux (MODE_SS, optional): a per-lane partial on entry, its wave sum
+// (lane63(wave_incl_scan), the same bits) on return -- reduced together with the SS (the DRAM chain
+// kernel's prior).
 template <int RPL, int NSEG, int MODE>
 __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>& e, int lane, double* lds,
                                             int64_t b, double* __restrict__ out0, double* __restrict__ out1,
-                                            int64_t ld_out) {
+                                            int64_t ld_out, double* aux = nullptr) {
   constexpr int SLOTS = 64 * RPL;      // rows 1..SLOTS (row 0 never holds a polymerase)
   // Simulated rows j = 0..SLOTS of each dye: simM[j] = lds[1 + j], simP[j] = lds[SLOTS + 3 + j],
   // so a lane's first row RPL*lane + 1 starts 16-B aligned (paired 16-B row stores).
@@ -305,6 +319,7 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
   }
 #endif
 
+  const double xt = kp.thr[lane];  // consumed by the distance cuts: the load overlaps the counter scan
   // ---- per-step setup: R_full = R + dR (SumofSquares...m:45); R<0 -> 0 (ConstantElongationSim.m:36)
   double prod[RPL];
   const unsigned ebits = max(max(max(exp_bits(v), exp_bits(tau)), max(exp_bits(ton), exp_bits(b1))),
@@ -321,6 +336,7 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
   }
   if (!fin || nonfinite != 0) {  // outside mcmcstat's finite parameter box: reported as NaN
     if (MODE != MODE_SS) write_nan<MODE>(lane, N, b, out0, out1, ld_out);
+    if (aux) *aux = lane63(wave_incl_scan(*aux));
     return NAN;
   }
 
@@ -328,9 +344,10 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
   double K[RPL];
   {
     double loc[RPL];
-    double s = 0.0;
+    double s = prod[0];  // (0.0 + prod[0] only turns a -0 into +0, which no count can see)
+    loc[0] = s;
 #pragma unroll
-    for (int q = 0; q < RPL; ++q) {
+    for (int q = 1; q < RPL; ++q) {
       s = s + prod[q];
       loc[q] = s;
     }
@@ -345,7 +362,8 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
       const double Sq = excl + loc[q];
       const double eps = Sq * 0x1p-42;  // >> the (g + 16) ulp bound between any two summation orders
       const double Kq = floor(Sq);
-      amb |= wave_ballot(Sq - eps < Kq) | wave_ballot(Sq + eps >= Kq + 1.0);  // an integer within eps of Sq
+      const double f = Sq - Kq;         // exact (Sterbenz): the fraction
+      amb |= wave_ballot(f < eps) | wave_ballot(f + eps >= 1.0);  // an integer within eps of Sq
       K[q] = Kq;
     }
     if ((kp.force_exact & 1) || amb != 0) {
@@ -394,7 +412,7 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
     // twice that at m = nsteps, precomputed per cell up to the factor v (CellMeta::eps_v).
     // No P_m equals a threshold unless it is within eps > 0 of it (then the wave goes exact),
     // so on the fast path #(P_m <= x) == #(P_m < x) and one count per threshold suffices.
-    if (fast) fast = distance_cuts<NSEG>(sm, sp, L, vd0, v * cm.eps_v, nsteps, lane, cu);
+    if (fast) fast = distance_cuts<NSEG>(xt, L, vd0, v * cm.eps_v, nsteps, lane, cu);
     if (fast) {
       // ---- {K, J} prefix tables (exact) and O(1) row sums
       double jloc[RPL], js = 0.0;
@@ -408,7 +426,7 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
           jloc[q] = js;
         }
       }
-      const double jexcl = wave_shr1(wave_incl_scan(js));
+      const double jexcl = wave_incl_scan(js) - js;  // integers < 2^53: exact, as a shifted scan
       // KJ[i], i in [-SLOTS-RPL, SLOTS): the SLOTS+RPL entries below i = 0 are zeros
       double2* KJ = reinterpret_cast<double2*>(lds) + SLOTS + RPL;
 #pragma unroll
@@ -562,6 +580,12 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
       const double r2 = pt[kk].y2 - pp;
       ss = fmax(fma(r2, r2, ss), ss);
     }
+  }
+  if (MODE == MODE_SS && aux) {
+    double x = *aux;
+    wave_incl_scan2(ss, x);
+    *aux = lane63(x);
+    return lane63(ss);
   }
   return MODE == MODE_SS ? lane63(wave_incl_scan(ss)) : 0.0;
 }

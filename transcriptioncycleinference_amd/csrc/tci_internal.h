@@ -50,6 +50,8 @@ struct KParams {
   const StepRec* steps;      // uniform grid t_interp (SumofSquares...m:30) and its steps
   const StepRec* steps_raw;  // raw times t and raw steps (forward on raw t, TranscriptionCycleMCMC.m:307)
   const PointRec* points;
+  const double* thr;         // 64 per-lane thresholds of the distance cuts (tci_eval.h distance_cuts): lane
+                             // 1 + 4k .. 4 + 4k = MS2 a, MS2 e, PP7 a, PP7 e of segment k; 0 elsewhere
   int64_t n_cells;
   int64_t cell_stride;       // records per cell in steps/steps_raw/points (64*(rows_per_lane+1); long cells: N_max
                              // rounded up to 64)

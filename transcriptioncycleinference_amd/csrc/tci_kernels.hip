@@ -246,7 +246,7 @@ __global__ __launch_bounds__(64) void tci_tile_kernel(const KParams kp, const do
   const double vd0 = v * cm.d;
   Cuts<NSEG> cu;
   // ---- distance cuts over m = 1..S and their exactness proof (as eval_wave)
-  if (v > 0.0 && fast) fast = distance_cuts<NSEG>(sm, sp, L, vd0, v * cm.eps_v, S, lane, cu);
+  if (v > 0.0 && fast) fast = distance_cuts<NSEG>(kp.thr[lane], L, vd0, v * cm.eps_v, S, lane, cu);
   if (v > 0.0 && fast) {
     // ---- O(1) row sums from the {K, J} tables, floors inside the segment loop, x A
     double kvdM[NSEG], kaM[NSEG], kvdP[NSEG], kaP[NSEG];
