@@ -176,10 +176,12 @@ void fill_segments(KParams* kp, const tci_construct* cs) {
     m.e = cs->ms2_end[s];
     m.phi = cs->ms2_loopn[s] / 24;  // GetFluorFromPolPos.m:48
     m.k = m.phi / (m.e - m.a);
+    m.ka = m.k * m.a;
     p.a = cs->pp7_start[s];
     p.e = cs->pp7_end[s];
     p.phi = cs->pp7_loopn[s] / 24;  // GetFluorFromPolPos.m:60
     p.k = p.phi / (p.e - p.a);
+    p.ka = p.k * p.a;
     kp->ms2[s] = m;
     kp->pp7[s] = p;
     emax = std::max(emax, std::max(m.e, p.e));

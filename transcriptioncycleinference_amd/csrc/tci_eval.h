@@ -146,36 +146,26 @@ __device__ __forceinline__ double occupancy(double p, const SegParams& s, double
 
 // Distance cut of one threshold x on the fast path: n(x) = #{m in [1, nsteps] : P_m < x}, where
 // P_m = m * vd0 is the representative position m steps after loading (P_m is monotone in m).
-// The cuts of all thresholds are computed at once, one threshold per lane, from x / vd0 and four
-// exact candidate products around it, instead of one vote per (slot, threshold):
-//   m_c = clamp(floor(x * rcp(vd0)) - 1, -2, nsteps + 1),  candidates m_c .. m_c + 3,
-//   n(x) = clamp(m_c - 1 + #{candidates with P_m < x}, 0, nsteps).
-// That count is exact whenever P_{m_c} < x (or m_c <= 0) and P_{m_c+3} >= x (or m_c + 3 > nsteps);
-// |x * rcp(vd0) - x / vd0| << 1 for every m that can matter, and a candidate set that does not
-// bracket x is flagged instead of trusted. `bad` also flags a candidate in [1, nsteps] within
-// eps of x: the same exactness test as one vote per m, because every other P_m is at least
-// ~vd0 > 4 eps away from x (eps >= vd0/4 is flagged too). A flagged wave takes the exact sweep.
+// The cuts of all thresholds are computed at once, one threshold per lane, from an estimate of
+// x / vd0 and the two exact products that should bracket x:
+//   m0 = clamp(ceil(x * rcp(vd0)) - 1, 0, nsteps),  n(x) = m0  when  P_{m0} < x <= P_{m0+1}
+// (m0 = 0 needs no lower product, m0 = nsteps no upper one). A pair that does not bracket x (the
+// estimate off by one: x / vd0 within ~1e-15 of an integer) is flagged instead of trusted. `bad`
+// also flags a bracketing product within eps of x: the same exactness test as one vote per m,
+// because every other P_m is at least ~vd0 > 4 eps away from x (eps >= vd0/4 is flagged too). A
+// flagged wave takes the exact sweep.
 __device__ __forceinline__ int distance_cut(double x, double vd0, double rvd0, double eps, int nsteps, bool& bad) {
   const double mf = x > 0.0 ? x * rvd0 : 0.0;  // x <= 0: no P_m (m >= 1) lies below it
-  double mc = floor(mf) - 1.0;
-  mc = mc > -2.0 ? mc : -2.0;
-  mc = mc < (double)(nsteps + 1) ? mc : (double)(nsteps + 1);  // also +Inf / NaN (rcp of a denormal)
+  double mc = ceil(mf) - 1.0;
+  mc = mc > 0.0 ? mc : 0.0;                                  // also NaN
+  mc = mc < (double)nsteps ? mc : (double)nsteps;            // also +Inf (rcp of a denormal)
   const int m0 = (int)mc;
-  int cnt = m0 - 1;
-  bool near = !(eps < 0.25 * vd0);
-  bool l0 = false, l3 = false;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int m = m0 + j;
-    const double P = (double)m * vd0;  // the same product as P_m = (g + 1) * vd0 per slot
-    const bool lt = P < x;
-    cnt += lt ? 1 : 0;
-    near = near | (m >= 1 && m <= nsteps && fabs(P - x) <= eps);
-    if (j == 0) l0 = lt;
-    if (j == 3) l3 = lt;
-  }
-  bad = near || (!l0 && m0 >= 1) || (l3 && m0 + 3 <= nsteps);
-  return min(max(cnt, 0), nsteps);
+  const double P0 = mc * vd0, P1 = (mc + 1.0) * vd0;         // the products P_m = (g + 1) * vd0 of the slots
+  const bool lo_ok = m0 == 0 || P0 < x;
+  const bool hi_ok = m0 == nsteps || !(P1 < x);
+  const bool near = !(eps < 0.25 * vd0) || (m0 >= 1 && fabs(P0 - x) <= eps) || (m0 < nsteps && fabs(P1 - x) <= eps);
+  bad = near || !lo_ok || !hi_ok;
+  return m0;
 }
 
 // Cuts of one evaluation (wave-uniform, SGPRs): nL = n(L); per segment and dye na = n(a), ne = n(e).
@@ -440,9 +430,9 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
 #pragma unroll
       for (int k = 0; k < NSEG; ++k) {
         kvdM[k] = sm[k].k * vd0;
-        kaM[k] = sm[k].k * sm[k].a;
+        kaM[k] = sm[k].ka;
         kvdP[k] = sp[k].k * vd0;
-        kaP[k] = sp[k].k * sp[k].a;
+        kaP[k] = sp[k].ka;
       }
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {

@@ -42,6 +42,7 @@ struct SegParams {
   double e;    // loop end (kb)
   double phi;  // loopn / 24
   double k;    // phi / (e - a): fractional-occupancy slope
+  double ka;   // k * a (the ramp's offset term of the fast-path row sums, theta-independent)
 };
 
 // Kernel arguments: device pointers of the resident cell table + the construct.

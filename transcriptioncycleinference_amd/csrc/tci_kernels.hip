@@ -253,9 +253,9 @@ __global__ __launch_bounds__(64) void tci_tile_kernel(const KParams kp, const do
 #pragma unroll
     for (int k = 0; k < NSEG; ++k) {
       kvdM[k] = sm[k].k * vd0;
-      kaM[k] = sm[k].k * sm[k].a;
+      kaM[k] = sm[k].ka;
       kvdP[k] = sp[k].k * vd0;
-      kaP[k] = sp[k].k * sp[k].a;
+      kaP[k] = sp[k].ka;
     }
     for (int r0 = 1; r0 <= S; r0 += 64) {
       const int r = r0 + lane;
