@@ -145,7 +145,7 @@ __device__ __forceinline__ double gamma_at(uint64_t seed, int64_t c, int64_t ste
 
 // Wave sum, result in every lane: DPP inclusive scan + lane 63 (tci_eval.h), no LDS round trips.
 // Every engine reduces through this one function, so their bits agree.
-__device__ __forceinline__ double wsum64(double x) { return lane63(wave_incl_scan(x)); }
+__device__ __forceinline__ double wsum64(double x) { return wave_sum(x); }
 
 // Lane l's value of x in every lane (readlane: scalar broadcast, l uniform).
 __device__ __forceinline__ double lane_bcast(double x, int l) {

@@ -83,9 +83,34 @@ __device__ __forceinline__ double wave_incl_scan(double x) {
   return x;
 }
 
+__device__ __forceinline__ double lane63(double x);
+
+// DPP move that writes every lane (row_mask 0xF, bound_ctrl: invalid sources read 0), so the old
+// value is dead and no zero-initialised destination is needed.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64_all(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+// The scan's value at lane 63 only (a wave sum), with the same adds in the same order there as
+// wave_incl_scan: the two cross-row stages update every row (rows 0-2 end up with other partial sums,
+// which no stage feeds into lane 63: lane 63 takes lane 47's row-2 total, then lane 31's rows-0..1
+// total), so their moves need no zeroed destination -- 4 fewer VALU per sum.
+__device__ __forceinline__ double wave_sum(double x) {
+  x = x + dpp_f64<0x111, 0xF>(x);
+  x = x + dpp_f64<0x112, 0xF>(x);
+  x = x + dpp_f64<0x114, 0xF>(x);
+  x = x + dpp_f64<0x118, 0xF>(x);
+  x = x + dpp_f64_all<0x142>(x);
+  x = x + dpp_f64_all<0x143>(x);
+  return lane63(x);
+}
+
 // Two independent scans stage by stage (each value's adds in wave_incl_scan's order, so the same
 // bits): the second one's DPP moves fill the first one's wait states.
-__device__ __forceinline__ void wave_incl_scan2(double& x, double& y) {
+__device__ __forceinline__ void wave_sum2(double& x, double& y) {  // wave_sum of both, interleaved
   x = x + dpp_f64<0x111, 0xF>(x);
   y = y + dpp_f64<0x111, 0xF>(y);
   x = x + dpp_f64<0x112, 0xF>(x);
@@ -94,10 +119,12 @@ __device__ __forceinline__ void wave_incl_scan2(double& x, double& y) {
   y = y + dpp_f64<0x114, 0xF>(y);
   x = x + dpp_f64<0x118, 0xF>(x);
   y = y + dpp_f64<0x118, 0xF>(y);
-  x = x + dpp_f64<0x142, 0xA>(x);
-  y = y + dpp_f64<0x142, 0xA>(y);
-  x = x + dpp_f64<0x143, 0xC>(x);
-  y = y + dpp_f64<0x143, 0xC>(y);
+  x = x + dpp_f64_all<0x142>(x);
+  y = y + dpp_f64_all<0x142>(y);
+  x = x + dpp_f64_all<0x143>(x);
+  y = y + dpp_f64_all<0x143>(y);
+  x = lane63(x);
+  y = lane63(y);
 }
 
 __device__ __forceinline__ double lane63(double x) {
@@ -126,6 +153,14 @@ template <int RPL>
 __device__ __forceinline__ uint64_t step_lanes(int nsteps, int q) {
   const int n = nsteps > q ? (nsteps - q + RPL - 1) / RPL : 0;
   return n >= 64 ? ~0ull : (1ull << n) - 1;
+}
+
+// max of two non-NaN doubles as one v_max_f64: fmax() makes the compiler canonicalise operands it
+// cannot prove canonical (values merged from several paths), one more VALU each.
+__device__ __forceinline__ double max_f64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
 
 // Exponent field of a double: all ones iff the value is +-Inf or NaN. The max over the
@@ -326,7 +361,7 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
   }
   if (!fin || nonfinite != 0) {  // outside mcmcstat's finite parameter box: reported as NaN
     if (MODE != MODE_SS) write_nan<MODE>(lane, N, b, out0, out1, ld_out);
-    if (aux) *aux = lane63(wave_incl_scan(*aux));
+    if (aux) *aux = wave_sum(*aux);
     return NAN;
   }
 
@@ -438,15 +473,18 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
       for (int q = 0; q < RPL; ++q) {
         const int r = RPL * lane + q + 1;
         const double rd = (double)r;
-        const double kL = KJ[r - cu.nL - 1].x;  // shared by every segment and dye (L_MS2 = L_PP7)
+        // entries r - n - 1 of this lane's rows as KJl[q - n]: one scalar offset per cut, the row
+        // in the instruction's immediate offset
+        const double2* KJl = KJ + RPL * lane;
+        const double kL = KJl[q - cu.nL].x;  // shared by every segment and dye (L_MS2 = L_PP7)
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) {
 #if TCI_ABLATE & 1
           accM[k][q] = KJ[r].x + (double)cu.nMa[k];
           accP[k][q] = KJ[r].y + (double)cu.nL;
 #else
-          accM[k][q] = row_sum(KJ, r, rd, cu.nMa[k], cu.nMe[k], kL, sm[k], kvdM[k], kaM[k]);
-          accP[k][q] = row_sum(KJ, r, rd, cu.nPa[k], cu.nPe[k], kL, sp[k], kvdP[k], kaP[k]);
+          accM[k][q] = row_sum(KJl, q + 1, rd, cu.nMa[k], cu.nMe[k], kL, sm[k], kvdM[k], kaM[k]);
+          accP[k][q] = row_sum(KJl, q + 1, rd, cu.nPa[k], cu.nPe[k], kL, sp[k], kvdP[k], kaP[k]);
 #endif
         }
         // one row's table reads in flight at a time: issued all at once, the 4*NSEG + 1 reads of
@@ -503,11 +541,11 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
 #pragma unroll
   for (int q = 0; q < RPL; ++q) {
     // MS2(MS2 < basal) = basal == max(MS2, basal): the sums are finite and >= 0 here
-    double m = fmax(accM[0][q], b1), pp = fmax(accP[0][q], b2);
+    double m = max_f64(accM[0][q], b1), pp = max_f64(accP[0][q], b2);
 #pragma unroll
     for (int k = 1; k < NSEG; ++k) {
-      m = fmax(m + accM[k][q], b1);
-      pp = fmax(pp + accP[k][q], b2);
+      m = max_f64(m + accM[k][q], b1);
+      pp = max_f64(pp + accP[k][q], b2);
     }
     rowM[q] = A * m;
     rowP[q] = pp;
@@ -573,11 +611,11 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
   }
   if (MODE == MODE_SS && aux) {
     double x = *aux;
-    wave_incl_scan2(ss, x);
-    *aux = lane63(x);
-    return lane63(ss);
+    wave_sum2(ss, x);
+    *aux = x;
+    return ss;
   }
-  return MODE == MODE_SS ? lane63(wave_incl_scan(ss)) : 0.0;
+  return MODE == MODE_SS ? wave_sum(ss) : 0.0;
 }
 
 }  // namespace
