@@ -308,7 +308,9 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
   const int64_t stride = ctx->rpl > 0 ? 64 * (ctx->rpl + 1) : (ctx->max_points + 63) / 64 * 64;
   ctx->stride = stride;
   const size_t total = (size_t)C * (size_t)stride;
-  std::vector<tci::StepRec> steps(total, tci::StepRec{0.0, 0.0}), steps_raw(total, tci::StepRec{0.0, 0.0});
+  // slots past a cell's last step: dt = 0 and t = -Inf, so every kernel skips them as steps before ton
+  // (ConstantElongationSim.m:57-60) without a bounds test
+  std::vector<tci::StepRec> steps(total, tci::StepRec{0.0, -INFINITY}), steps_raw(total, tci::StepRec{0.0, -INFINITY});
   std::vector<tci::PointRec> points(total, tci::PointRec{NAN, NAN, NAN, 0, 0});
   ctx->grid.assign(total, 0.0);
   for (int64_t c = 0; c < C; ++c) {

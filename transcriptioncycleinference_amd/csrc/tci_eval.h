@@ -190,16 +190,17 @@ __device__ __forceinline__ double occupancy(double p, const SegParams& s, double
 // because every other P_m is at least ~vd0 > 4 eps away from x (eps >= vd0/4 is flagged too). A
 // flagged wave takes the exact sweep.
 __device__ __forceinline__ int distance_cut(double x, double vd0, double rvd0, double eps, int nsteps, bool& bad) {
-  const double mf = x > 0.0 ? x * rvd0 : 0.0;  // x <= 0: no P_m (m >= 1) lies below it
-  double mc = ceil(mf) - 1.0;
-  mc = mc > 0.0 ? mc : 0.0;                                  // also NaN
-  mc = mc < (double)nsteps ? mc : (double)nsteps;            // also +Inf (rcp of a denormal)
+  // x <= 0 (no P_m with m >= 1 below it): x * rvd0 <= 0, or NaN for 0 * Inf, and the clamp gives 0
+  double mc = ceil(x * rvd0) - 1.0;
+  mc = fmax(mc, 0.0);                    // also NaN (v_max_f64 returns the other operand)
+  mc = fmin(mc, (double)nsteps);         // also +Inf (rcp of a denormal)
   const int m0 = (int)mc;
   const double P0 = mc * vd0, P1 = (mc + 1.0) * vd0;         // the products P_m = (g + 1) * vd0 of the slots
-  const bool lo_ok = m0 == 0 || P0 < x;
-  const bool hi_ok = m0 == nsteps || !(P1 < x);
-  const bool near = !(eps < 0.25 * vd0) || (m0 >= 1 && fabs(P0 - x) <= eps) || (m0 < nsteps && fabs(P1 - x) <= eps);
-  bad = near || !lo_ok || !hi_ok;
+  // bitwise, not short-circuit: straight-line lane masks (no branch, no mask rebuilt for the vote)
+  const bool lo_ok = (m0 == 0) | (P0 < x);
+  const bool hi_ok = (m0 == nsteps) | !(P1 < x);
+  const bool near = !(eps < 0.25 * vd0) | ((m0 >= 1) & (fabs(P0 - x) <= eps)) | ((m0 < nsteps) & (fabs(P1 - x) <= eps));
+  bad = near | !lo_ok | !hi_ok;
   return m0;
 }
 
@@ -237,7 +238,8 @@ __device__ __forceinline__ bool distance_cuts(double xt, double L, double vd0, d
 //   K_i = sum_{i' <= i} c_i'        (= floor(counter_i): polymerases loaded through step i)
 //   J_i = sum_{i' <= i} i' * c_i'
 // Both are integers < 2^53, exact in any summation order. KJ points at i = 0 of a table whose
-// SLOTS+RPL entries below i = 0 are zeros, so every index r - m - 1 >= -SLOTS needs no clamp.
+// SLOTS entries below i = 0 are zeros (of SLOTS+RPL reserved), so every index r - m - 1 >= -SLOTS
+// needs no clamp.
 // CLAMP (the long-cell kernel): the table has ONE zero entry below i = 0 and lower indices read it.
 template <bool CLAMP = false>
 __device__ __forceinline__ double2 kj_at(const double2* KJ, int i) { return KJ[CLAMP ? max(i, -1) : i]; }
@@ -284,8 +286,10 @@ struct EvalIn {
   double v, tau, ton, b1, b2, A, R;  // wave-uniform
   double dr[RPL];                     // dR of the lane's steps RPL*lane + q (any value past N-1)
   CellMeta cm;
+  double thr;                         // this lane's distance-cut threshold (KParams::thr)
   StepRec st[RPL];
-  PointRec pt[RPL + 1];               // points lane + 64*k (the last one only for lane 0)
+  PointRec pt[RPL + 1];               // points lane + 64*k, k < RPL; pt[RPL]: point 64*RPL in every lane
+                                      // (wave-uniform; only N = 64*RPL + 1 has it, and lane 0 uses it)
 };
 
 // The cell's records into registers: lane l holds steps RPL*l .. RPL*l + RPL - 1 and points
@@ -297,14 +301,15 @@ __device__ __forceinline__ void load_cell(const KParams& kp, int c, int lane, Ev
   const StepRec* ST = (RAW ? kp.steps_raw : kp.steps) + cbase;
   const PointRec* PT = kp.points + cbase;
   e.cm = kp.cells[c];
+  e.thr = kp.thr[lane];  // with the cell's loads (a load at its use would wait there)
 #pragma unroll
   for (int q = 0; q < RPL; ++q) e.st[q] = ST[RPL * lane + q];  // < cell_stride
   if (!RAW) {
 #pragma unroll
     for (int k = 0; k <= RPL; ++k) {
       const int j = lane + 64 * k;
-      if (k < RPL || j <= 64 * RPL) e.pt[k] = PT[j];
-      else e.pt[k] = PointRec{NAN, NAN, NAN, 0, 0};  // beyond every cell's points: dropped
+      // the tail point at a uniform address: scalar loads, no per-lane defaults to materialise
+      e.pt[k] = PT[k < RPL ? j : 64 * RPL];
     }
   }
 }
@@ -344,7 +349,6 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
   }
 #endif
 
-  const double xt = kp.thr[lane];  // consumed by the distance cuts: the load overlaps the counter scan
   // ---- per-step setup: R_full = R + dR (SumofSquares...m:45); R<0 -> 0 (ConstantElongationSim.m:36)
   double prod[RPL];
   const unsigned ebits = max(max(max(exp_bits(v), exp_bits(tau)), max(exp_bits(ton), exp_bits(b1))),
@@ -353,11 +357,11 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
   uint64_t nonfinite = 0;
 #pragma unroll
   for (int q = 0; q < RPL; ++q) {
-    const int g = RPL * lane + q;
-    const bool valid = g < nsteps;
     nonfinite |= step_lanes<RPL>(nsteps, q) & wave_ballot(!isfinite(dr[q]));
     const double rho = fmax(R + dr[q], 0.0);  // R(R<0) = 0 (the sign of a zero cannot reach floor())
-    prod[q] = (valid && !(st[q].t < ton)) ? rho * st[q].dt : 0.0;  // skipped steps add nothing (:57-60)
+    // skipped steps add nothing (:57-60); slots past the last step have t = -Inf (tci_create), so
+    // they are skipped too, whatever dR holds there
+    prod[q] = !(st[q].t < ton) ? rho * st[q].dt : 0.0;
   }
   if (!fin || nonfinite != 0) {  // outside mcmcstat's finite parameter box: reported as NaN
     if (MODE != MODE_SS) write_nan<MODE>(lane, N, b, out0, out1, ld_out);
@@ -421,15 +425,20 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
   }
   const double L = kp.L0 + tau * v;                 // L_MS2 = L_PP7 (GetFluorFromPolPos.m:19-20), no FMA
   const double pstop = L > kp.emax ? L : kp.emax;  // f(p) == 0 for every p >= pstop
+  // Row sums per segment: assigned by the fast path, accumulated from 0 by the exact sweep, 0 for
+  // v <= 0 (zeroed in those branches only: no zero moves on the fast path).
   double accM[NSEG][RPL], accP[NSEG][RPL];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int q = 0; q < RPL; ++q)
+    for (int q = 0; q < RPL; ++q)
 #pragma unroll
-    for (int k = 0; k < NSEG; ++k) accM[k][q] = accP[k][q] = 0.0;
+      for (int k = 0; k < NSEG; ++k) accM[k][q] = accP[k][q] = 0.0;
+  };
 
-  // v <= 0: every position stays <= 0 <= loop start, so no polymerase is ever lit.
-  if (v > 0.0) {
-    bool fast = MODE != MODE_FWD_RAW && !(kp.force_exact & 2);
+  // v <= 0: every position stays <= 0 <= loop start, so no polymerase is ever lit (the exact
+  // branch's zeros, without the sweep).
+  {
+    bool fast = v > 0.0 && MODE != MODE_FWD_RAW && !(kp.force_exact & 2);
     const double vd0 = v * cm.d;
     Cuts<NSEG> cu;
     // ---- distance cuts and their exactness proof (distance_cut)
@@ -437,7 +446,7 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
     // twice that at m = nsteps, precomputed per cell up to the factor v (CellMeta::eps_v).
     // No P_m equals a threshold unless it is within eps > 0 of it (then the wave goes exact),
     // so on the fast path #(P_m <= x) == #(P_m < x) and one count per threshold suffices.
-    if (fast) fast = distance_cuts<NSEG>(xt, L, vd0, v * cm.eps_v, nsteps, lane, cu);
+    if (fast) fast = distance_cuts<NSEG>(e.thr, L, vd0, v * cm.eps_v, nsteps, lane, cu);
     if (fast) {
       // ---- {K, J} prefix tables (exact) and O(1) row sums
       double jloc[RPL], js = 0.0;
@@ -452,13 +461,12 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
         }
       }
       const double jexcl = wave_incl_scan(js) - js;  // integers < 2^53: exact, as a shifted scan
-      // KJ[i], i in [-SLOTS-RPL, SLOTS): the SLOTS+RPL entries below i = 0 are zeros
+      // KJ[i], i in [-SLOTS-RPL, SLOTS): the SLOTS entries below i = 0 are zeros
       double2* KJ = reinterpret_cast<double2*>(lds) + SLOTS + RPL;
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {
         KJ[RPL * lane + q] = make_double2(K[q], jexcl + jloc[q]);
-        KJ[RPL * lane + q - SLOTS - RPL] = make_double2(0.0, 0.0);
-        if (lane == 0) KJ[q - RPL] = make_double2(0.0, 0.0);
+        KJ[RPL * lane + q - SLOTS] = make_double2(0.0, 0.0);  // [-SLOTS, 0): every index a row reads
       }
       wave_sync();
       double kvdM[NSEG], kaM[NSEG], kvdP[NSEG], kaP[NSEG];
@@ -494,7 +502,9 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
       }
     } else {
       // ---- exact systolic sweep: at iteration s slot g holds cohort g-s+1 with its forward position
+      zero_acc();
       double cc[RPL], p[RPL], vd[RPL];
+      if (v > 0.0) {
       {
         const double kprev = wave_shr1(K[RPL - 1]);
 #pragma unroll
@@ -531,6 +541,7 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
         }
         if (alive == 0) break;
       }
+      }  // v > 0
     }
   }
   wave_sync();  // every {K,J}-table read is done before the rows overwrite the LDS
@@ -596,11 +607,11 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
     const double m = fma(w, simM[k + 1] - simM[k], simM[k]);
     const double pp = fma(w, simP[k + 1] - simP[k], simP[k]);
     if (MODE == MODE_FWD_INTERP) {
-      if (j < N) {
+      if (j < N) {  // the tail (kk == RPL): lane 0 only
         out0[b * ld_out + j] = m;
         out1[b * ld_out + j] = pp;
       }
-    } else {
+    } else if (kk < RPL || lane == 0) {  // the tail point is every lane's pt[RPL]: lane 0 adds it
       // nansum drops NaN data, NaN simulation and the all-NaN padding points (j >= N) alike:
       // fma(r, r, ss) >= ss unless it is NaN, and max() returns the non-NaN operand.
       const double r1 = pt[kk].y1 - m;

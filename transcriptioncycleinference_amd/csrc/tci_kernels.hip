@@ -39,11 +39,14 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
     if (lane == 0) out0[b] = INFINITY;  // skipped proposal (bounds-rejected by the caller)
     return;
   }
-  if (c < 0 || c >= kp.n_cells) {
+  if (c < 0 || ((kp.n_cells >> 31) == 0 && c >= (int)kp.n_cells)) {
     write_nan<MODE>(lane, 0, b, out0, out1, ld_out);
     return;
   }
   const double* th = theta + b * ld;
+  // the row length in 32 bits (ld > 0): the lanes' index compares and the row check in 32-bit
+  // (scalar) compares instead of 64-bit vector ones
+  const int ldi = (ld >> 31) != 0 ? 0x7fffffff : (int)ld;
   EvalIn<RPL> e;
   load_cell<RPL, MODE == MODE_FWD_RAW>(kp, c, lane, e);
   e.v = th[0];
@@ -60,12 +63,12 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
 #pragma unroll
     for (int q = 0; q < RPL; q += 2) {
       const int g = RPL * lane + q;
-      if (8 + g < ld) {
+      if (8 + g < ldi) {
         const d2u x = *reinterpret_cast<const d2u*>(th + 7 + g);
         e.dr[q] = x.x;
         e.dr[q + 1] = x.y;
       } else {
-        e.dr[q] = 7 + g < ld ? th[7 + g] : 0.0;
+        e.dr[q] = 7 + g < ldi ? th[7 + g] : 0.0;
         e.dr[q + 1] = 0.0;
       }
     }
@@ -73,11 +76,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
 #pragma unroll
     for (int q = 0; q < RPL; ++q) {
       const int g = RPL * lane + q;
-      e.dr[q] = 7 + g < ld ? th[7 + g] : 0.0;  // speculative (N unknown yet), kept inside the row
+      e.dr[q] = 7 + g < ldi ? th[7 + g] : 0.0;  // speculative (N unknown yet), kept inside the row
     }
   }
   const int N = e.cm.n;
-  if (ld < 7 + N) {  // a row shorter than 7 + N entries
+  if (ldi < 7 + N) {  // a row shorter than 7 + N entries
     write_nan<MODE>(lane, N, b, out0, out1, ld_out);
     return;
   }
