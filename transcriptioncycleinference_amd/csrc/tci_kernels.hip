@@ -10,9 +10,12 @@ namespace {
 // budget for 6 waves/SIMD: 50 vs 58 us per launch at the compiler's default 5; 7-8 no faster.
 // (An XCD-aware block -> row-range order measured ~1 % slower: the cell table fits every XCD's L2.)
 constexpr int kWavesPerBlock = 4;
+#ifndef TCI_LK_WPE
+#define TCI_LK_WPE 6  // waves per SIMD the register budget is set for (A/B: scripts/ab_variants.py)
+#endif
 
 template <int RPL, int NSEG, int MODE>
-__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(6))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
+__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(TCI_LK_WPE))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
