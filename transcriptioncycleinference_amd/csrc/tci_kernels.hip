@@ -6,16 +6,21 @@ namespace tci {
 
 namespace {
 
-// 4 independent waves per 256-thread block (1- and 8-wave blocks measured no faster). Register
-// budget for 6 waves/SIMD: 50 vs 58 us per launch at the compiler's default 5; 7-8 no faster.
+// 4 independent waves per 256-thread block (1- and 8-wave blocks measured no faster). Round 2: a
+// register budget for 6 waves/SIMD took 50 vs 58 us per launch at the compiler's default 5, and 7-8
+// were no faster then; with round 3's shorter instruction stream 8 pays (below).
 // (An XCD-aware block -> row-range order measured ~1 % slower: the cell table fits every XCD's L2.)
 constexpr int kWavesPerBlock = 4;
+// Waves per SIMD the register budget is set for: 8 while RPL * NSEG <= 2 (58 VGPRs at RPL = 2,
+// NSEG = 1, no spill; 34.4 vs 36.0 us per bench launch against 6 in one process,
+// profiles/r03_likelihood/r03occ1_ab.json; 7: 35.8), 6 above (RPL = 2 with two segments spills at
+// 8; the LDS of a 4-wave block caps RPL = 4 at 4 waves/SIMD anyway).
 #ifndef TCI_LK_WPE
-#define TCI_LK_WPE 6  // waves per SIMD the register budget is set for (A/B: scripts/ab_variants.py)
+#define TCI_LK_WPE(RPL, NSEG) ((RPL) * (NSEG) <= 2 ? 8 : 6)
 #endif
 
 template <int RPL, int NSEG, int MODE>
-__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(TCI_LK_WPE))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
+__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(TCI_LK_WPE(RPL, NSEG)))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
