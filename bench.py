@@ -559,9 +559,22 @@ def main():
             dist.init_process_group(backend, rank=rank, world_size=world, device_id=torch.device("cuda", device_index))
         else:
             dist.init_process_group(backend, rank=rank, world_size=world)
+    if not rehearsal and local >= visible_devices():
+        print(f"bench.py: rank {rank} has LOCAL_RANK {local} but only {visible_devices()} GPU(s) are visible",
+              file=sys.stderr)
+        sys.exit(2)
     dev = torch.device("cuda", device_index)
     torch.cuda.set_device(dev)
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
+    ident = dict(device_identity(device_index), rank=rank, local_rank=local)
+    if distributed:
+        idents = [None] * world
+        dist.all_gather_object(idents, ident)
+        pcis = [d["pci"] for d in idents]
+        if not rehearsal and len(set(pcis)) != world:
+            raise RuntimeError(f"bench.py: {world} ranks share {len(set(pcis))} GPU(s): {pcis}")
+    else:
+        idents = [ident]
 
     def reduce(x, op):
         if not distributed:
@@ -627,6 +640,7 @@ def main():
                 f"; 1 {'RCCL' if backend == 'nccl' else 'gloo'} gather after timing)" if distributed else ")"),
             "launcher": os.environ.get("TCI_BENCH_LAUNCHER") or ("torch.distributed.run" if distributed else "none"),
             "kernel_rows_per_lane": lk.info["rows_per_lane"],
+            "devices": idents,
         },
         "roofline": {
             "bound": "hbm",
@@ -713,6 +727,36 @@ def _free_port() -> int:
     return port
 
 
+def visible_devices() -> int:
+    """GPUs this process may use, counted WITHOUT initialising the GPU (torch.cuda.device_count()
+    reads the device list without creating a HIP context on this image), so the parent can refuse
+    a --gpus N it cannot honour before any child touches a GPU."""
+    forced = os.environ.get("TCI_BENCH_DEVICES")  # CPU tests of the launcher only
+    if forced:
+        return int(forced)
+    import torch
+
+    return int(torch.cuda.device_count())
+
+
+def check_devices(gpus: int, visible: int, rehearsal: bool):
+    """A run on N GPUs needs N visible devices (one rank per GPU); the one-GPU rehearsal needs 1.
+    Raises LaunchError instead of silently running several ranks on one device."""
+    need = 1 if rehearsal else gpus
+    if visible < need:
+        raise LaunchError(f"--gpus {gpus} needs {need} visible GPU(s), found {visible} "
+                          f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES', '<unset>')})")
+
+
+def device_identity(device_index: int) -> dict:
+    """This rank's device as the driver's record can check it: PCI domain:bus:device and name."""
+    import torch
+
+    pr = torch.cuda.get_device_properties(device_index)
+    return {"device_index": device_index, "pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}",
+            "name": pr.name, "gcn_arch": getattr(pr, "gcnArchName", "")}
+
+
 def launch_plan(gpus: int, env: dict, port: int = 0):
     """How this invocation runs. None: in this process (a launcher such as torch.distributed.run set
     WORLD_SIZE, or one GPU). Otherwise one environment per rank for ``gpus`` child processes:
@@ -765,6 +809,10 @@ def entry() -> int:
     known, _ = ap.parse_known_args()
     try:
         plan = launch_plan(known.gpus, dict(os.environ))
+        if not {"-h", "--help"} & set(sys.argv[1:]) and (plan is not None or int(os.environ.get("WORLD_SIZE", "1")) == 1):
+            # the parent (or a lone process) refuses before anything initialises a GPU; a rank
+            # started by an outside launcher checks its own LOCAL_RANK in main()
+            check_devices(known.gpus, visible_devices(), os.environ.get("TCI_BENCH_REHEARSAL") == "1")
     except LaunchError as e:
         print(f"bench.py: {e}", file=sys.stderr)
         return 2

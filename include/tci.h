@@ -154,7 +154,8 @@ typedef struct {
   int64_t thin;         /* keep every thin-th chain row in outputs.chain (0 = keep none) */
   uint64_t seed;
   int32_t engine;       /* TCI_DRAM_AUTO / _FUSED / _BATCHED / _WALK (below) */
-  int32_t reserved;
+  int32_t max_chunk;    /* FUSED/WALK: at most this many chain rows per draws pass + walk (0 = automatic:
+                           adaptint, or the draws buffer's 2 GiB cap); same chains whatever it is */
   const int64_t* chain_keys; /* optional [n_chains]: chain c draws from RNG stream chain_keys[c]
                                 (NULL: stream c). Keying chains by their global cell index makes a
                                 shard of a run (its cells on one GPU) reproduce the unsharded chains */

@@ -35,12 +35,7 @@
 #define OR_EARG -3
 #define OR_ENOMEM -4
 
-typedef struct {
-  double L0;
-  int32_t n_seg;
-  const double *ms2_start, *ms2_end, *ms2_loopn;
-  const double *pp7_start, *pp7_end, *pp7_loopn;
-} or_construct;
+#include "tci_oracle.h"
 
 static double round_half_away(double x) { return x >= 0 ? floor(x + 0.5) : -floor(-x + 0.5); }
 
@@ -228,6 +223,21 @@ static int ss_one(const or_construct *cs, const double *t, const double *y1, con
   }
   *ss_out = ss;
   return OR_OK;
+}
+
+/* One SS evaluation with caller-held scratch (the DRAM restatement's ssfun, oracle/tci_dram_oracle.c). */
+void *oracle_scratch_new(int64_t cap) {
+  scratch *w = (scratch *)malloc(sizeof(scratch));
+  if (!w) return NULL;
+  if (scratch_init(w, cap) != OR_OK) { scratch_free(w); free(w); return NULL; }
+  return w;
+}
+void oracle_scratch_free(void *w) {
+  if (w) { scratch_free((scratch *)w); free(w); }
+}
+int oracle_ss_one(const or_construct *cs, const double *t, const double *y1, const double *y2, int64_t N,
+                  const double *th, void *w, double *ss_out) {
+  return ss_one(cs, t, y1, y2, N, th, (scratch *)w, ss_out);
 }
 
 /* Batched SS: ss_out[b] = ssfun(theta[b,:], cell[cell_id[b]]); inactive rows get +Inf.

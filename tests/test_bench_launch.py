@@ -49,13 +49,41 @@ def test_mismatch_exits_nonzero_before_any_gpu_work():
 
 def test_spawned_ranks_run_and_exit_cleanly():
     # every child gets WORLD_SIZE=2, so it runs main() itself: --help exits 0 before touching torch
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--help"], env=_env(),
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--help"],
+                       env=_env(TCI_BENCH_DEVICES="2"),
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.count("usage:") == 2
 
 
 def test_a_failing_rank_fails_the_launch():
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-such-flag"], env=_env(),
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--no-such-flag"],
+                       env=_env(TCI_BENCH_DEVICES="2"),
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
+
+
+@pytest.mark.parametrize("gpus,visible,rehearsal,ok", [(8, 8, False, True), (8, 7, False, False), (2, 1, False, False),
+                                                       (2, 1, True, True), (1, 0, False, False)])
+def test_device_count_check(gpus, visible, rehearsal, ok):
+    if ok:
+        bench.check_devices(gpus, visible, rehearsal)
+    else:
+        with pytest.raises(bench.LaunchError):
+            bench.check_devices(gpus, visible, rehearsal)
+
+
+def test_too_few_devices_refused_before_any_rank_starts():
+    # the parent counts devices (torch.cuda.device_count(): no HIP context) and exits 2; no child runs
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"], env=_env(TCI_BENCH_DEVICES="4"),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2
+    assert "needs 8 visible GPU(s), found 4" in r.stderr
+    assert "usage:" not in r.stdout
+
+
+def test_no_gpu_refused_for_one_rank():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")], env=_env(TCI_BENCH_DEVICES="0"),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2
+    assert "needs 1 visible GPU(s), found 0" in r.stderr

@@ -264,6 +264,59 @@ def test_fused_and_batched_engines_give_identical_chains(lk, ntry):
     assert np.median(a.accept_rate) > 0.01
 
 
+STATS_CASES = {  # (n_steps, adaptint, burnintime, stats_from, max_chunk)
+    "stats_from_mid_window_partial_last": (437, 100, 200, 150, 0),
+    "no_adaptation": (300, 0, 100, 77, 0),
+    "window_spans_chunks": (437, 100, 200, 150, 30),
+    "every_row": (250, 100, 100, 1, 0),
+    "stats_from_last_row": (305, 100, 100, 305, 0),
+}
+
+
+@pytest.mark.parametrize("engine", ["fused", "walk", "batched"])
+@pytest.mark.parametrize("case", sorted(STATS_CASES))
+def test_posterior_summaries_equal_the_chain_rows(lk, engine, case):
+    """The on-device summaries (window sums merged pairwise, carried across chunks) against the raw
+    rows (thin = 1): mean(chain(stats_from:end, :)) and std(., 1) (TranscriptionCycleMCMC.m:284-301),
+    sqrt(mean(s2chain)) and std(sqrt(s2chain), 1) (:302-303) over every row -- with stats_from inside
+    a window, a partial last window, no adaptation (window = chunk), a window split over several
+    chain-kernel launches (max_chunk < adaptint) and a one-row statistics range."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions
+
+    n_steps, ai, burn, sf, mc = STATS_CASES[case]
+    ids = list(range(3, 299, 23))
+    o = DramOptions(n_steps=n_steps, adaptint=ai, burnintime=burn, stats_from=sf, thin=1, seed=41, engine=engine,
+                    max_chunk=mc)
+    res, _ = run(lk, ids, o)
+    n = lk.cells.lengths[ids]
+    assert res.chain.shape[0] == n_steps
+    for k in range(len(ids)):
+        P = 7 + int(n[k])
+        X = res.chain[sf - 1:, k, :P]
+        scale = np.abs(X).max(axis=0) + 1.0
+        np.testing.assert_allclose(res.mean[k, :P], X.mean(axis=0), rtol=0, atol=1e-12 * scale.max(), err_msg=case)
+        np.testing.assert_allclose(res.std[k, :P], X.std(axis=0), rtol=0, atol=1e-10 * scale.max(), err_msg=case)
+        q = np.sqrt(res.s2chain[:, k])
+        np.testing.assert_allclose(res.sigma_mean[k], np.sqrt(res.s2chain[:, k].mean()), rtol=1e-12, err_msg=case)
+        np.testing.assert_allclose(res.sigma_std[k], q.std(), rtol=1e-9, atol=1e-12 * q.max(), err_msg=case)
+    assert np.median(res.accept_rate) > 0.01
+
+
+@pytest.mark.parametrize("engine", ["fused", "walk"])
+def test_chunk_size_does_not_change_the_chains(lk, engine):
+    """The fused engines' chunking (draws pass + walk per chunk) is invisible in the chains: a run
+    whose windows span several chunks equals the one-chunk-per-window run bit for bit."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions
+
+    ids = list(range(0, 299, 29))
+    o = DramOptions(n_steps=437, burnintime=200, adaptint=100, stats_from=150, thin=3, seed=5, engine=engine)
+    a, _ = run(lk, ids, o)
+    o.max_chunk = 17
+    b, _ = run(lk, ids, o)
+    for f in ("chain", "s2chain", "mean", "std", "final_theta", "sigma_mean", "sigma_std", "accept_rate", "n_evals"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+
+
 @pytest.mark.parametrize("engine", ["fused", "batched"])
 def test_adapted_proposal_is_the_scaled_chain_covariance(lk, engine):
     """mcmcstat's adaptation: after the last adaptation row n (n >= burnintime), the proposal
@@ -593,3 +646,34 @@ def test_walk_at_10000_chains_equals_fused_and_batched():
         np.testing.assert_array_equal(o.n_evals, w.n_evals, err_msg=eng)
         np.testing.assert_array_equal([r["mean_v"] for r in o.MCMCresults], [r["mean_v"] for r in w.MCMCresults],
                                       err_msg=eng)
+
+
+@pytest.mark.parametrize("engine", ["fused", "walk", "batched"])
+def test_gpu_chains_follow_the_cpu_restatement(lk, c_oracle, construct, engine):
+    """The GPU sampler against the CPU restatement of mcmcstat's DRAM (oracle/tci_dram_oracle.c, the
+    C oracle as ssfun, mcmcstat's own MATLAB-form expressions: divisions by sigma2, the alpha13
+    quotient, R./drscale, covupd's row recurrence, a textbook Cholesky) on the same Philox streams:
+    both chains take the same accept / reject decisions at every step, through burn-in scaling and
+    covariance adaptation, and their rows agree to the rounding of the continuous arithmetic."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions, dram_run, plan_fit
+
+    ids = [0, 41, 97, 150, 222, 298]
+    plan = plan_fit(lk.cells, ids, 3)
+    o = DramOptions(n_steps=600, burnintime=300, adaptint=100, stats_from=200, thin=1, seed=77, engine=engine)
+    keys = np.array(plan.cells, np.int64)
+    g = dram_run(lk, np.array(plan.cells, np.int32), plan.x0, plan.lower, plan.upper, plan.prior_mu, plan.prior_sig,
+                 plan.qcov_diag, 1.0, o, chain_keys=keys)
+    c = c_oracle.dram_run(lk.cells, construct, np.array(plan.cells, np.int32), plan.x0, plan.lower, plan.upper,
+                          plan.prior_mu, plan.prior_sig, plan.qcov_diag, 1.0, o, keys=keys, want_chain=True)
+    n = lk.cells.lengths[ids]
+    for k in range(len(ids)):
+        P = 7 + int(n[k])
+        G, Cc = g.chain[:, k, :P], c["chain"][:, k, :P]
+        moved_g = np.any(G[1:] != G[:-1], axis=1)
+        moved_c = np.any(Cc[1:] != Cc[:-1], axis=1)
+        np.testing.assert_array_equal(moved_g, moved_c, err_msg=f"chain {k}: accept/reject decisions differ")
+        np.testing.assert_allclose(G, Cc, rtol=1e-9, atol=1e-9, err_msg=f"chain {k}")
+        np.testing.assert_allclose(g.s2chain[:, k], c["s2chain"][:, k], rtol=1e-9)
+        assert g.n_evals[k] == c["n_evals"][k]
+    np.testing.assert_allclose(g.mean, c["mean"], rtol=1e-9, atol=1e-9)
+    assert np.median(g.accept_rate) > 0.02

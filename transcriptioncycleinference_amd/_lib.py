@@ -59,7 +59,7 @@ class tci_dram_options(C.Structure):
     _fields_ = [("n_steps", C.c_int64), ("burnintime", C.c_int64), ("adaptint", C.c_int64), ("ntry", C.c_int32),
                 ("updatesigma", C.c_int32), ("drscale", C.c_double), ("adascale", C.c_double),
                 ("qcovadj", C.c_double), ("burnin_scale", C.c_double), ("stats_from", C.c_int64),
-                ("thin", C.c_int64), ("seed", C.c_uint64), ("engine", C.c_int32), ("reserved", C.c_int32),
+                ("thin", C.c_int64), ("seed", C.c_uint64), ("engine", C.c_int32), ("max_chunk", C.c_int32),
                 ("chain_keys", C.POINTER(C.c_int64))]
 
 

@@ -601,7 +601,7 @@ int tci_dram_defaults(tci_dram_options* o) {
   o->thin = 0;
   o->seed = 20201028;
   o->engine = TCI_DRAM_AUTO;
-  o->reserved = 0;
+  o->max_chunk = 0;
   o->chain_keys = nullptr;
   return TCI_OK;
 }
@@ -615,9 +615,10 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
       !qcov_diag || !sigma2_0)
     return fail(ctx, TCI_EINVAL, "tci_dram_run: null argument or no chains");
   if (opt->n_steps < 1 || opt->ntry < 1 || opt->ntry > 2 || opt->adaptint < 0 || !(opt->drscale > 0) ||
-      opt->engine < TCI_DRAM_AUTO || opt->engine > TCI_DRAM_WALK)
+      opt->engine < TCI_DRAM_AUTO || opt->engine > TCI_DRAM_WALK || opt->max_chunk < 0)
     return fail(ctx, TCI_EINVAL,
-                "tci_dram_run: bad options (n_steps >= 1, ntry in {1,2}, adaptint >= 0, engine in {0,1,2,3})");
+                "tci_dram_run: bad options (n_steps >= 1, ntry in {1,2}, adaptint >= 0, engine in {0,1,2,3}, "
+                "max_chunk >= 0)");
   int rc = check_rows(ctx, ld, cell_id, n_chains);
   if (rc != TCI_OK) return rc;
   if (ld > TCI_MAX_POINTS + 7) return fail(ctx, TCI_ERANGE, "tci_dram_run: ld too large");
@@ -646,7 +647,8 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   const int64_t ai = opt->adaptint;
   const int64_t DW = tci::draw_stride(ld);
   const int64_t chunk_cap = std::max<int64_t>(32, (int64_t)(((size_t)2 << 30) / (n * (size_t)DW * sizeof(double))));
-  const int64_t chunk = std::min<int64_t>(ai > 0 ? ai : 1000, chunk_cap);
+  int64_t chunk = std::min<int64_t>(ai > 0 ? ai : 1000, chunk_cap);
+  if (opt->max_chunk > 0) chunk = std::min<int64_t>(chunk, opt->max_chunk);
   const int64_t win = ai > 0 ? ai : chunk;
   const int64_t n_keep = opt->thin > 0 ? (opt->n_steps + opt->thin - 1) / opt->thin : 0;
   st.n_chains = n_chains;

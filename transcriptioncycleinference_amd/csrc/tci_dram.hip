@@ -1063,9 +1063,13 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     qa.S2 = cont ? st.s2acc[3 * c + 2] : 0.0;
     qa.K = ca.first > 1 ? st.sq_mean[c] : sqrt(st.s2log[c * p.win]);
   }
-  auto rec_row = [&](int64_t row, const double* x) {
+  // Stores and sums of the records are split: the window sums are added before the barrier (as the
+  // rows are decided), the log/thinned-output STORES go out at the top of the next round, before
+  // that round's candidate loads. The stores are then older than every load a round waits for, so
+  // the round's vmcnt waits (the compiler merges the store counts of the uniform branches into
+  // vmcnt(0)) find them long completed instead of waiting ~1-3 k cycles for fresh store acks.
+  auto store_row = [&](int64_t row, const double* x) {
     log_row<NJ>(st, p, c, slot0 + row, P, x, lane);
-    ca.add(row, x);
     int64_t k;
     if (st.chain_out != nullptr && kept_row(p, row, k)) {
 #pragma unroll
@@ -1073,32 +1077,66 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
         if (lane + 64 * q < P) st.chain_out[(k * st.n_chains + c) * ld + lane + 64 * q] = x[q];
     }
   };
-  auto rec_s2 = [&](int64_t row, double v) {  // lane 0
-    log_s2(st, p, c, slot0 + row, v);
-    qa.add(v);
-    int64_t k;
-    if (st.s2_out != nullptr && kept_row(p, row, k)) st.s2_out[k * st.n_chains + c] = v;
-  };
-  auto flush_vec = [&]() {  // unrolled: a bounded store count (a runtime loop made the compiler
-                            // wait for every store before the next round's loads were used)
+  // kRecWave: rows prow .. prow + padv - 1 (decided by the previous round; all but the last kept
+  // the state thp)
+  auto store_vec = [&]() {  // unrolled: a bounded store count
 #pragma unroll
     for (int i = 0; i < D - 1; ++i)
-      if (i + 1 < padv) rec_row(prow + i, thp);  // uniform
-    if (padv >= 1) rec_row(prow + padv - 1, th);
+      if (i + 1 < padv) store_row(prow + i, thp);  // uniform
+    if (padv >= 1) store_row(prow + padv - 1, th);
   };
-  auto flush_s2 = [&](double x0) {
+  auto acc_vec = [&]() {
+#pragma unroll
+    for (int i = 0; i < D - 1; ++i)
+      if (i + 1 < padv) ca.add(prow + i, thp);  // uniform
+    if (padv >= 1) ca.add(prow + padv - 1, th);
+  };
+  // kSigWave, lane 0: the s2 of rows s2row .. s2row + s2n - 1, summed when known (acc_s2, one round
+  // after the rows are decided), stored at the top of the following round (store_s2)
+  int64_t s2row = 0;
+  int s2n = 0;
+  double s2v[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) s2v[i] = 0.0;
+  auto store_s2 = [&]() {
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        if (i < s2n) {  // uniform
+          log_s2(st, p, c, slot0 + s2row + i, s2v[i]);
+          int64_t k;
+          if (st.s2_out != nullptr && kept_row(p, s2row + i, k)) st.s2_out[k * st.n_chains + c] = s2v[i];
+        }
+      }
+    }
+  };
+  auto acc_s2 = [&](double x0) {  // the rows prow .. prow + padv - 1; x0: the s2 of the last
     if (lane == 0) {
 #pragma unroll
       for (int i = 0; i < D - 1; ++i)
-        if (i + 1 < padv) rec_s2(prow + i, s2f[i]);
-      if (padv >= 1) rec_s2(prow + padv - 1, x0);
+        if (i + 1 < padv) qa.add(s2f[i]);
+      if (padv >= 1) qa.add(x0);
     }
+#pragma unroll
+    for (int i = 0; i < D - 1; ++i) s2v[i] = i + 1 < padv ? s2f[i] : x0;
+    s2v[D - 1] = x0;
+    s2row = prow;
+    s2n = padv;
   };
+  // the loop-carried loads land before the loop: at the loop head only the previous round's
+  // stores can be in flight, so no wait inside a round depends on how many were issued
+#pragma unroll
+  for (int q = 0; q < EPW; ++q)
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) asm volatile("" ::"v"(ucur[q][k]));
+  asm volatile("" ::"v"(dsc));
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = stamp(), t1;
 #define TCI_PHASE(k) \
   if (TCI_CHAIN_PROFILE) { t1 = stamp(); ph[k] += t1 - t0; t0 = t1; }
   for (int64_t s = s_begin; s <= s_end; par ^= 1) {
     launder_lane(lane);
+    if (w == kRecWave) store_vec();  // the rows the previous round decided
+    if (w == kSigWave) store_s2();   // the s2 of the rows decided two rounds ago
     // ---- this wave's proposals, their bounds (wave vote) and evaluations
 #pragma unroll
     for (int q = 0; q < EPW; ++q) {
@@ -1167,14 +1205,14 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       const double ipv = 1.0 / x;
       if (lane < D) xip[par][lane] = ipv;
       const double x0 = lane_bcast(x, 0);
-      flush_s2(x0);
+      acc_s2(x0);
       s2c = x0;
       gpend = false;
 #pragma unroll
       for (int i = 0; i < D - 1; ++i) s2f[i] = lane_bcast(x, i + 1);  // the s2 of row s + i if unmoved
     }
-    if (w == kRecWave) flush_vec();
     if (w == kRecWave) {
+      acc_vec();
 #pragma unroll
       for (int k = 0; k < NJ; ++k) thp[k] = th[k];  // the state before this round's rows
     }
@@ -1242,7 +1280,9 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     // s + adv + a1 + 2q is candidate adv + 2q - 1), or a load now
 #pragma unroll
     for (int q = 0; q < EPW; ++q) {
-      bool have = false;
+      // EPW = 1: adv is 1 or 2 and both candidates are prefetched (no load_u path, so ucur never
+      // has a load in flight at the loop head)
+      bool have = EPW == 1;
 #pragma unroll
       for (int i = 0; i < NPF; ++i) have = have || adv + 2 * q - 1 == kPf[i];
       if (have) {  // uniform
@@ -1275,7 +1315,8 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 #endif
   // the last round's rows
   if (w == kRecWave) {
-    flush_vec();
+    store_vec();
+    acc_vec();
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
       const int j = lane + 64 * k;
@@ -1305,7 +1346,9 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   }
   if (w == kSigWave) {
     const double x0 = (p.updatesigma && gpend) ? 1.0 / (Gl * (2.0 / ss)) : s2c;
-    flush_s2(x0);
+    store_s2();  // the previous round's rows
+    acc_s2(x0);
+    store_s2();  // the last round's rows
     if (lane == 0) {
       st.sigma2[c] = x0;
       if (with_records) {

@@ -55,6 +55,7 @@ class DramOptions:
     thin: int = 0
     seed: int = 20201028
     engine: str = "auto"          # "auto" | "fused" | "batched" | "walk" (include/tci.h TCI_DRAM_*): identical chains
+    max_chunk: int = 0            # FUSED/WALK rows per draws pass + walk (0 = automatic); identical chains
 
     ENGINES = {"auto": 0, "fused": 1, "batched": 2, "walk": 3}
 
@@ -66,7 +67,7 @@ class DramOptions:
                                      int(bool(self.updatesigma)), float(self.drscale), float(self.adascale),
                                      float(self.qcovadj), float(self.burnin_scale), int(self.stats_from),
                                      int(self.thin), int(self.seed) & 0xFFFFFFFFFFFFFFFF,
-                                     self.ENGINES[self.engine], 0, _lib.ptr(chain_keys, _lib._i64p))
+                                     self.ENGINES[self.engine], int(self.max_chunk), _lib.ptr(chain_keys, _lib._i64p))
 
 
 @dataclass
