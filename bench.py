@@ -230,6 +230,7 @@ def end_to_end(lk, n_steps: int, seed: int, reduce=None):
         evals, chains = int(reduce(evals, "sum")), int(reduce(chains, "sum"))
     return {"n_steps": n_steps, "chains": chains, "device_s": dev_s, "wall_s": wall,
             "ssfun_evals": evals, "value": evals / wall, "unit": "SS evals/s (wall time, SURVEY §8(d)(ii))",
+            "value_basis": "wall",
             "us_per_step": wall * 1e6 / max(n_steps - 1, 1),
             "device_value": evals / dev_s, "device_us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
             "accept_rate_median_rank0": float(np.median(fr.accept_rate))}
@@ -343,6 +344,7 @@ def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_s
                        + ("" if n_steps >= 200000 else " (bounded sample of the configured 200k)"),
            "n_steps": n_steps, "engine": engine, "chains": int(reduce(len(fr.MCMCresults), "sum")), "device_s": dev_s,
            "wall_s": wall, "ssfun_evals": evals, "value": evals / wall, "unit": "SS evals/s (wall time)",
+           "value_basis": "wall",
            "scaling": "strong", "us_per_step": wall * 1e6 / max(n_steps - 1, 1),
            "device_value": evals / dev_s, "device_us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
            "accept_rate_median_rank0": float(np.median(fr.accept_rate)),
@@ -364,7 +366,8 @@ def cpu_baseline_synth(cfg: int, spot: dict, seconds: float):
     ac = np.ones(len(ci), np.uint8)
     threads = c_oracle.max_threads()
     want, st = c_oracle.ss_batch(cells.offsets, cells.t, cells.ms2, cells.pp7, cs, th, ci)
-    rel = float(np.max(np.abs(spot["ss_gpu"] - want) / np.abs(want))) if np.all(st == 0) else float("nan")
+    rel = float(np.max(np.abs(spot["ss_gpu"] - want) / np.maximum(np.abs(want), 1e-300))) if np.all(st == 0) \
+        else float("nan")
     rate, evals, reps, el = _cpu_rate(cells, cs, th, ci, ac, threads, seconds)
     one = np.arange(min(len(ci), 64))
     rate1, evals1, reps1, el1 = _cpu_rate(cells, cs, th[one], ci[one], ac[one], 1, seconds / 2)
@@ -375,6 +378,47 @@ def cpu_baseline_synth(cfg: int, spot: dict, seconds: float):
                             "sample": f"{len(one)} rows x {reps1} passes = {evals1} evals in {el1:.1f} s"},
             "oracle_spot_check": {"rows": int(len(ci)), "max_rel_err_gpu_vs_oracle": rel,
                                   "ok": bool(rel <= 1e-6), "tolerance": 1e-6}}
+
+
+def cpu_fit_config1(lk, n_steps: int = 10000, n_burn: int = 1000, seed: int = 1):
+    """BASELINE config 1 as written: TestData cell 1, n_steps = 10,000,
+    n_burn = 1,000, fitted on the host -- mcmcstat's DRAM restated in C with the C oracle as ssfun
+    (oracle/tci_dram_oracle.c, one chain, one core: mcmcstat's loop is serial) -- the CPU counterpart
+    of mode (ii). The same cell is fitted on the GPU with the same inputs (x0, bounds, J0, seed, RNG
+    streams: mcmc.fit), and the posterior summaries of v and R are compared: the two samplers take
+    the same decisions on the same streams, so they agree far inside the posterior sd."""
+    from oracle import c_oracle, oracle as ref  # cpu_baseline leg only
+    from transcriptioncycleinference_amd.mcmc import DramOptions, fit, plan_fit
+
+    c_oracle.build()
+    cell = 0
+    g0 = time.perf_counter()
+    fr = fit(lk, n_steps=n_steps, n_burn=n_burn, seed=seed, cells=[cell])
+    g_wall = time.perf_counter() - g0
+    plan = plan_fit(lk.cells, [cell], seed)
+    o = DramOptions(n_steps=n_steps, burnintime=n_burn, stats_from=max(n_burn, 1), seed=seed * 1000003 + 20201028)
+    t0 = time.perf_counter()
+    r = c_oracle.dram_run(lk.cells, ref.builtin_construct(CONSTRUCT), np.array(plan.cells, np.int32), plan.x0,
+                          plan.lower, plan.upper, plan.prior_mu, plan.prior_sig, plan.qcov_diag, 1.0, o,
+                          keys=np.array(plan.cells, np.int64), nthreads=1)
+    wall = time.perf_counter() - t0
+    evals = int(r["n_evals"][0])
+    g = fr.MCMCresults[0]
+    cmp = {}
+    for name, j in (("v", 0), ("R", 6)):
+        mc, sc, mg, sg = float(r["mean"][0, j]), float(r["std"][0, j]), g["mean_" + name], g["sigma_" + name]
+        cmp[name] = {"cpu_mean": mc, "gpu_mean": mg, "cpu_sd": sc, "gpu_sd": sg,
+                     "mean_diff_in_sd": abs(mc - mg) / max(sc, 1e-300), "sd_rel_diff": abs(sc - sg) / max(sc, 1e-300)}
+    ok = all(c["mean_diff_in_sd"] < 3.0 and c["sd_rel_diff"] < 0.5 for c in cmp.values())
+    return {"value": evals / wall, "unit": "SS evals/s (wall time, one chain)", "cores": 1, "kind": "port",
+            "sample": f"BASELINE config 1 in full: TestData cell 1, {n_steps} steps, n_burn {n_burn}, {evals} ssfun "
+                      f"evals in {wall:.2f} s; mcmcstat's DRAM restated in C (oracle/tci_dram_oracle.c) with the C "
+                      f"matrix-form oracle as ssfun, one core",
+            "us_per_step": wall * 1e6 / max(n_steps - 1, 1), "wall_s": wall,
+            "gpu_same_fit": {"wall_s": g_wall, "us_per_step": g_wall * 1e6 / max(n_steps - 1, 1),
+                             "ssfun_evals": int(fr.n_evals), "note": "one chain on the GPU: latency-bound, the "
+                             "GPU's throughput needs many chains (end_to_end_dram)"},
+            "posterior_check": cmp, "posterior_check_ok": bool(ok)}
 
 
 def hierarchical_end_to_end(lk, n_steps: int, seed: int, reduce):
@@ -391,7 +435,7 @@ def hierarchical_end_to_end(lk, n_steps: int, seed: int, reduce):
     wall = reduce(time.perf_counter() - t0, "max")
     dev_s, evals = reduce(fr.elapsed_ms * 1e-3, "max"), int(reduce(fr.n_evals, "sum"))
     return {"n_steps": n_steps, "chains": int(reduce(len(fr.MCMCresults), "sum")), "device_s": dev_s, "wall_s": wall,
-            "ssfun_evals": evals, "value": evals / wall, "unit": "SS evals/s (wall time)",
+            "ssfun_evals": evals, "value": evals / wall, "unit": "SS evals/s (wall time)", "value_basis": "wall",
             "us_per_step": wall * 1e6 / max(n_steps - 1, 1),
             "device_value": evals / dev_s, "device_us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
             "v_fixed": bool(all(abs(r["mean_v"] - v0[int(r["cell_index"]) - 1]) <= 1e-5 + 1e-12
@@ -693,6 +737,7 @@ def main():
                                                                             args.synth_dram_steps, reduce)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cells, theta_h, rounds_cid(cells, args.proposals), act_h, args.cpu_seconds)
+        res["cpu_fit_config1"] = cpu_fit_config1(lk)
         for cfg, spot in spots.items():
             res[f"cpu_baseline_config{cfg}"] = cpu_baseline_synth(cfg, spot, args.cpu_seconds / 2)
     if rank == 0:

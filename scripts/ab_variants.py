@@ -2,7 +2,8 @@
 """A/B timing of kernel build variants, interleaved in ONE process (cdna_hip_programming.md
 §5.4 rule 24). Build here:  python scripts/ab_variants.py --build
 Run on the GPU box:         python scripts/ab_variants.py --run [--rounds 9 --launches 20]
-Every variant is also checked against the shipped build (rel <= 1e-12)."""
+Every variant is also checked against the first one: bit for bit (`bitwise_equal_to_first`,
+`rows_differing_in_bits`) and, separately, to 1e-12 relative (`rel_vs_first`)."""
 import argparse
 import json
 import os
@@ -94,14 +95,19 @@ def run(names, rounds, launches, proposals):
     res = {}
     for n in names:
         got = outs[n].cpu().numpy()
-        rr = np.abs(got - ref) / np.abs(ref)
+        rr = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-300)
         rr[~act] = 0
         rel = float(np.nanmax(rr))
+        # bit-for-bit agreement (NaN == NaN) reported apart from the 1e-12 relative check
+        same = (got.view(np.uint64) == ref.view(np.uint64)) | (np.isnan(got) & np.isnan(ref))
+        bits_equal = bool(np.all(same))
+        n_diff_bits = int((~same).sum())
         bad = np.nonzero(~(rr <= 1e-12))[0]
         if len(bad):
             print(n, "mismatching rows", len(bad), "first", [(int(i), int(cid[i]), float(ref[i]), float(got[i])) for i in bad[:8]], file=sys.stderr)
         t = np.array(times[n])
         res[n] = {"median_us": float(np.median(t)), "min_us": float(t.min()), "rel_vs_first": rel,
+                  "bitwise_equal_to_first": bits_equal, "rows_differing_in_bits": n_diff_bits,
                   "evals_per_s": float(act.sum() / (np.median(t) * 1e-6)), "defines": VARIANTS.get(n)}
     print(json.dumps(res, indent=1))
 

@@ -563,6 +563,16 @@ struct DevAllocs {
   }
 };
 
+// Chain groups of the fused engines (tci_dram_run): TCI_DRAM_GROUPS (1..kMaxGroups) overrides the
+// default of one group.
+constexpr int kMaxGroups = 8;
+int dram_groups(int64_t n_chains) {
+  int g = 1;
+  if (const char* v = std::getenv("TCI_DRAM_GROUPS")) g = std::atoi(v);
+  g = std::max(1, std::min(g, kMaxGroups));
+  return (int)std::min<int64_t>(g, std::max<int64_t>(n_chains, 1));
+}
+
 // One DRAM step: propose -> ssfun -> accept/propose stage 2 -> ssfun -> accept, sigma2, log the row
 // -> [window records] -> [adapt] -> step + 1.
 int enqueue_step(tci_ctx* ctx, const tci::DramState& st, const tci::DramParams& p, hipStream_t s, bool with_stats,
@@ -643,16 +653,21 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   tci::DramParams p{};
   // Chunk of chain rows per fused-engine pass (its draws buffer holds one chunk; at most the next
   // adaptation row) and the window slots per chain: the covupd window (adaptint rows), which is also
-  // the fused engines' per-row log of a chunk; without adaptation the log holds one chunk.
+  // every engine's per-row log.
   const int64_t ai = opt->adaptint;
   const int64_t DW = tci::draw_stride(ld);
   const int64_t chunk_cap = std::max<int64_t>(32, (int64_t)(((size_t)2 << 30) / (n * (size_t)DW * sizeof(double))));
-  int64_t chunk = std::min<int64_t>(ai > 0 ? ai : 1000, chunk_cap);
+  // Without adaptation the window is 100 rows: the records' merge partition (the same for every engine)
+  // and the batched engine's graph block stay small (a 1,000-row window made the batched engine run up
+  // to 1,000 steps as plain launches before its first graph replay).
+  const int64_t win = ai > 0 ? ai : 100;
+  int64_t chunk = std::min<int64_t>(win, chunk_cap);
   if (opt->max_chunk > 0) chunk = std::min<int64_t>(chunk, opt->max_chunk);
-  const int64_t win = ai > 0 ? ai : chunk;
   const int64_t n_keep = opt->thin > 0 ? (opt->n_steps + opt->thin - 1) / opt->thin : 0;
   st.n_chains = n_chains;
   st.ld = ld;
+  st.c0 = 0;
+  st.c1 = n_chains;
 #define TCI_ALLOC(field, T, count)                                  \
   do {                                                              \
     st.field = A.alloc<T>((count), &e);                             \
@@ -711,10 +726,10 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(s2sum, double, n);
   TCI_ALLOC(sq_mean, double, n);
   TCI_ALLOC(sq_m2, double, n);
-  TCI_ALLOC(step, int64_t, 1);
+  TCI_ALLOC(step, int64_t, kMaxGroups);  // one step counter per chain group
 #if defined(TCI_CHAIN_PROFILE) || defined(TCI_ADAPT_PROFILE)
-  TCI_ALLOC(prof, int64_t, 8);
-  TCI_HIP(ctx, hipMemsetAsync(st.prof, 0, 8 * sizeof(int64_t), ctx->stream));
+  TCI_ALLOC(prof, int64_t, 32);
+  TCI_HIP(ctx, hipMemsetAsync(st.prof, 0, 32 * sizeof(int64_t), ctx->stream));
 #endif
   if (n_keep > 0 && (out->chain || out->s2chain)) {
     TCI_ALLOC(chain_out, double, (size_t)n_keep * n * L);
@@ -763,8 +778,8 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
     TCI_HIP(ctx, hipMemcpyAsync(st.step, &one, sizeof(int64_t), hipMemcpyHostToDevice, s));
     if ((rc = tci::dram_launch_stats(st, p, s)) != TCI_OK) return fail(ctx, rc, "dram stats launch");
   }
-  const int64_t two = 2;
-  TCI_HIP(ctx, hipMemcpyAsync(st.step, &two, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  const int64_t two[kMaxGroups] = {2, 2, 2, 2, 2, 2, 2, 2};
+  TCI_HIP(ctx, hipMemcpyAsync(st.step, two, sizeof(two), hipMemcpyHostToDevice, s));
   hipEvent_t ev0, ev1;
   TCI_HIP(ctx, hipEventCreate(&ev0));
   TCI_HIP(ctx, hipEventCreate(&ev1));
@@ -799,14 +814,46 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
     p.chunk = chunk;
     st.draws = A.alloc<double>(n * (size_t)p.chunk * DW, &e);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dram draws)");
-    for (int64_t next = 2; next <= opt->n_steps && rc == TCI_OK;) {
+    // Chain groups: the chains split into G contiguous groups, each walking its chunks on its own
+    // stream (its own step counter), group g starting once group g - 1 has walked its first chunk,
+    // so one group's walk overlaps another's draws and adaptation. Every chain's kernels and inputs
+    // are the same, so the chains are identical for any G.
+    const int G = dram_groups(n_chains);
+    std::vector<hipStream_t> gs(G, s);
+    std::vector<hipEvent_t> gev(G, nullptr);
+    std::vector<tci::DramState> gst(G, st);
+    for (int g = 0; g < G; ++g) {
+      gst[g].c0 = (int64_t)g * n_chains / G;
+      gst[g].c1 = (int64_t)(g + 1) * n_chains / G;
+      gst[g].step = st.step + g;
+      if (g > 0 && e == hipSuccess) e = hipStreamCreateWithFlags(&gs[g], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&gev[g], hipEventDisableTiming);
+    }
+    if (e == hipSuccess && G > 1) e = hipEventRecord(gev[0], s);  // the other streams start after the setup
+    for (int g = 1; g < G && e == hipSuccess; ++g) e = hipStreamWaitEvent(gs[g], gev[0], 0);
+    for (int64_t next = 2; next <= opt->n_steps && rc == TCI_OK && e == hipSuccess;) {
       int64_t end = std::min<int64_t>(opt->n_steps, next + p.chunk - 1);
       end = std::min<int64_t>(end, ((next + win - 1) / win) * win);  // chunks never cross a window
       const int rec = end % win == 0 || end == opt->n_steps;  // the records kept in the chain kernel
-      rc = tci::dram_launch_chain(st, p, ctx->kp, ctx->rpl, next, end, rec, s);
-      if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(st, p, s);
+      for (int g = 0; g < G && rc == TCI_OK && e == hipSuccess; ++g) {
+        rc = tci::dram_launch_chain(gst[g], p, ctx->kp, ctx->rpl, next, end, rec, gs[g]);
+        if (next == 2 && g + 1 < G && rc == TCI_OK) {  // group g + 1 follows group g's first walk
+          e = hipEventRecord(gev[g], gs[g]);
+          if (e == hipSuccess) e = hipStreamWaitEvent(gs[g + 1], gev[g], 0);
+        }
+        if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(gst[g], p, gs[g]);
+      }
       next = end + 1;
     }
+    for (int g = 1; g < G; ++g) {  // join
+      if (e == hipSuccess) e = hipEventRecord(gev[g], gs[g]);
+      if (e == hipSuccess) e = hipStreamWaitEvent(s, gev[g], 0);
+    }
+    for (int g = 0; g < G; ++g) {
+      if (gev[g]) (void)hipEventDestroy(gev[g]);
+      if (g > 0 && gs[g] != s) (void)hipStreamDestroy(gs[g]);
+    }
+    if (e != hipSuccess) return hip_fail(ctx, e, "DRAM chain groups");
     e = hipSuccess;
   } else {
   // The step loop. Steps 2 .. n_steps; adaptation after steps that are multiples of adaptint.
@@ -852,18 +899,21 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   if (graph) (void)hipGraphDestroy(graph);
 #if defined(TCI_CHAIN_PROFILE) || defined(TCI_ADAPT_PROFILE)
   {
-    int64_t ph[8];
+    int64_t ph[32];
     TCI_HIP(ctx, hipMemcpy(ph, st.prof, sizeof(ph), hipMemcpyDeviceToHost));
     // TCI_CHAIN_PROFILE=1: slots 0-6 are wave 0's cycles per phase; slot 5 also counts the rounds
     // in its bits 40+ (decoded here). =2: per-wave barrier waits (0-3) and pre-barrier work (4-7).
     // TCI_ADAPT_PROFILE: thread 0's cycles per adaptation phase. All summed over the chains.
     double rounds = 0.0;
-#if defined(TCI_CHAIN_PROFILE) && TCI_CHAIN_PROFILE == 1
+    int nslots = 8;
+#if defined(TCI_CHAIN_PROFILE) && (TCI_CHAIN_PROFILE == 1 || TCI_CHAIN_PROFILE == 3)
+    // =3: slots 8 w + k, wave w's cycles per phase (slot 8 w + 5 also counts the rounds)
+    nslots = TCI_CHAIN_PROFILE == 3 ? 32 : 8;
     rounds = (double)((uint64_t)ph[5] >> 40) / (double)n;
-    ph[5] = (int64_t)((uint64_t)ph[5] & ((1ull << 40) - 1));
+    for (int w = 0; w < nslots / 8; ++w) ph[8 * w + 5] = (int64_t)((uint64_t)ph[8 * w + 5] & ((1ull << 40) - 1));
 #endif
     std::fprintf(stderr, "{\"cycles_per_chain\": [");
-    for (int k = 0; k < 8; ++k) std::fprintf(stderr, "%s%.1f", k ? ", " : "", (double)ph[k] / (double)n);
+    for (int k = 0; k < nslots; ++k) std::fprintf(stderr, "%s%.1f", k ? ", " : "", (double)ph[k] / (double)n);
     std::fprintf(stderr, "], \"rounds_per_chain\": %.1f}\n", rounds);
   }
 #endif

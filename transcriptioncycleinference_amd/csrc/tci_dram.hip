@@ -679,8 +679,8 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
   constexpr int kDrawWaves = NWD, kDrawThreads = 64 * NWD;
   constexpr int kDrawCT = CT;
   extern __shared__ __attribute__((aligned(16))) double dyn[];
-  const int64_t c = blockIdx.x;
-  if (c >= st.n_chains) return;
+  const int64_t c = st.c0 + blockIdx.x;
+  if (c >= st.c1) return;
   const int64_t ld = st.ld;
   const int L = (int)ld;
   const int P = st.npar[c];
@@ -780,7 +780,10 @@ template <int NJ>
 struct ColAcc {
   double ws[NJ], S1[NJ], S2[NJ], K[NJ];
   int64_t first, sf;
-  bool kfirst;  // no statistics row before the window: K = the window's first row
+  bool kfirst;  // no statistics row before the window: K = the window's first statistics row (row sf:
+                // a sample of the rows summed, so S2 - S1^2/nb cancels no more than a variance does; the
+                // window's first row, which may precede stats_from, gave a chain stuck far from it an M2
+                // of rounding noise, even negative)
   __device__ void setup(const DramParams& p, int64_t row) {
     first = win_first(p, row);
     sf = max(first, p.stats_from);
@@ -793,7 +796,7 @@ struct ColAcc {
   __device__ __forceinline__ void add(int64_t row, const double* x) {
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
-      if (kfirst && row == first) K[k] = x[k];
+      if (kfirst && row == sf) K[k] = x[k];
       ws[k] = ws[k] + x[k];
       if (row >= sf) {
         const double d = x[k] - K[k];
@@ -981,8 +984,8 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   __shared__ double yl[2][NS][64 * NJ];                         // by round parity: every proposal
   __shared__ double xch[2][NS][4];                              // by round parity: ss, prior, in-bounds
   __shared__ double xip[2][D];                                  // by round parity: precisions of steps s + h
-  const int64_t c = blockIdx.x;
-  if (c >= st.n_chains) return;
+  const int64_t c = st.c0 + blockIdx.x;
+  if (c >= st.c1) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int lane = threadIdx.x & 63;  // re-laundered every round (launder_lane)
   const int64_t ld = st.ld;
@@ -1054,7 +1057,9 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       ca.ws[k] = cont && in ? st.wsumv[c * ld + j] : 0.0;
       ca.S1[k] = cont && in ? st.wacc1[c * ld + j] : 0.0;
       ca.S2[k] = cont && in ? st.wacc2[c * ld + j] : 0.0;
-      ca.K[k] = !in ? 0.0 : !ca.kfirst ? st.smean[c * ld + j] : cont ? st.window[c * p.win * ld + j] : 0.0;
+      // a window continued from an earlier chunk whose row sf is already logged: K = that row
+      ca.K[k] = !in ? 0.0 : !ca.kfirst ? st.smean[c * ld + j]
+                                         : ca.sf < s_begin ? st.window[(c * p.win + log_slot(p, ca.sf)) * ld + j] : 0.0;
     }
   }
   if (w == kSigWave) {
@@ -1063,13 +1068,9 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     qa.S2 = cont ? st.s2acc[3 * c + 2] : 0.0;
     qa.K = ca.first > 1 ? st.sq_mean[c] : sqrt(st.s2log[c * p.win]);
   }
-  // Stores and sums of the records are split: the window sums are added before the barrier (as the
-  // rows are decided), the log/thinned-output STORES go out at the top of the next round, before
-  // that round's candidate loads. The stores are then older than every load a round waits for, so
-  // the round's vmcnt waits (the compiler merges the store counts of the uniform branches into
-  // vmcnt(0)) find them long completed instead of waiting ~1-3 k cycles for fresh store acks.
-  auto store_row = [&](int64_t row, const double* x) {
+  auto rec_row = [&](int64_t row, const double* x) {
     log_row<NJ>(st, p, c, slot0 + row, P, x, lane);
+    ca.add(row, x);
     int64_t k;
     if (st.chain_out != nullptr && kept_row(p, row, k)) {
 #pragma unroll
@@ -1077,66 +1078,32 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
         if (lane + 64 * q < P) st.chain_out[(k * st.n_chains + c) * ld + lane + 64 * q] = x[q];
     }
   };
-  // kRecWave: rows prow .. prow + padv - 1 (decided by the previous round; all but the last kept
-  // the state thp)
-  auto store_vec = [&]() {  // unrolled: a bounded store count
+  auto rec_s2 = [&](int64_t row, double v) {  // lane 0
+    log_s2(st, p, c, slot0 + row, v);
+    qa.add(v);
+    int64_t k;
+    if (st.s2_out != nullptr && kept_row(p, row, k)) st.s2_out[k * st.n_chains + c] = v;
+  };
+  auto flush_vec = [&]() {  // unrolled: a bounded store count (a runtime loop made the compiler
+                            // wait for every store before the next round's loads were used)
 #pragma unroll
     for (int i = 0; i < D - 1; ++i)
-      if (i + 1 < padv) store_row(prow + i, thp);  // uniform
-    if (padv >= 1) store_row(prow + padv - 1, th);
+      if (i + 1 < padv) rec_row(prow + i, thp);  // uniform
+    if (padv >= 1) rec_row(prow + padv - 1, th);
   };
-  auto acc_vec = [&]() {
-#pragma unroll
-    for (int i = 0; i < D - 1; ++i)
-      if (i + 1 < padv) ca.add(prow + i, thp);  // uniform
-    if (padv >= 1) ca.add(prow + padv - 1, th);
-  };
-  // kSigWave, lane 0: the s2 of rows s2row .. s2row + s2n - 1, summed when known (acc_s2, one round
-  // after the rows are decided), stored at the top of the following round (store_s2)
-  int64_t s2row = 0;
-  int s2n = 0;
-  double s2v[D];
-#pragma unroll
-  for (int i = 0; i < D; ++i) s2v[i] = 0.0;
-  auto store_s2 = [&]() {
-    if (lane == 0) {
-#pragma unroll
-      for (int i = 0; i < D; ++i) {
-        if (i < s2n) {  // uniform
-          log_s2(st, p, c, slot0 + s2row + i, s2v[i]);
-          int64_t k;
-          if (st.s2_out != nullptr && kept_row(p, s2row + i, k)) st.s2_out[k * st.n_chains + c] = s2v[i];
-        }
-      }
-    }
-  };
-  auto acc_s2 = [&](double x0) {  // the rows prow .. prow + padv - 1; x0: the s2 of the last
+  auto flush_s2 = [&](double x0) {
     if (lane == 0) {
 #pragma unroll
       for (int i = 0; i < D - 1; ++i)
-        if (i + 1 < padv) qa.add(s2f[i]);
-      if (padv >= 1) qa.add(x0);
+        if (i + 1 < padv) rec_s2(prow + i, s2f[i]);
+      if (padv >= 1) rec_s2(prow + padv - 1, x0);
     }
-#pragma unroll
-    for (int i = 0; i < D - 1; ++i) s2v[i] = i + 1 < padv ? s2f[i] : x0;
-    s2v[D - 1] = x0;
-    s2row = prow;
-    s2n = padv;
   };
-  // the loop-carried loads land before the loop: at the loop head only the previous round's
-  // stores can be in flight, so no wait inside a round depends on how many were issued
-#pragma unroll
-  for (int q = 0; q < EPW; ++q)
-#pragma unroll
-    for (int k = 0; k < NJ; ++k) asm volatile("" ::"v"(ucur[q][k]));
-  asm volatile("" ::"v"(dsc));
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = stamp(), t1;
 #define TCI_PHASE(k) \
   if (TCI_CHAIN_PROFILE) { t1 = stamp(); ph[k] += t1 - t0; t0 = t1; }
   for (int64_t s = s_begin; s <= s_end; par ^= 1) {
     launder_lane(lane);
-    if (w == kRecWave) store_vec();  // the rows the previous round decided
-    if (w == kSigWave) store_s2();   // the s2 of the rows decided two rounds ago
     // ---- this wave's proposals, their bounds (wave vote) and evaluations
 #pragma unroll
     for (int q = 0; q < EPW; ++q) {
@@ -1205,14 +1172,14 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       const double ipv = 1.0 / x;
       if (lane < D) xip[par][lane] = ipv;
       const double x0 = lane_bcast(x, 0);
-      acc_s2(x0);
+      flush_s2(x0);
       s2c = x0;
       gpend = false;
 #pragma unroll
       for (int i = 0; i < D - 1; ++i) s2f[i] = lane_bcast(x, i + 1);  // the s2 of row s + i if unmoved
     }
+    if (w == kRecWave) flush_vec();
     if (w == kRecWave) {
-      acc_vec();
 #pragma unroll
       for (int k = 0; k < NJ; ++k) thp[k] = th[k];  // the state before this round's rows
     }
@@ -1280,9 +1247,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     // s + adv + a1 + 2q is candidate adv + 2q - 1), or a load now
 #pragma unroll
     for (int q = 0; q < EPW; ++q) {
-      // EPW = 1: adv is 1 or 2 and both candidates are prefetched (no load_u path, so ucur never
-      // has a load in flight at the loop head)
-      bool have = EPW == 1;
+      bool have = false;
 #pragma unroll
       for (int i = 0; i < NPF; ++i) have = have || adv + 2 * q - 1 == kPf[i];
       if (have) {  // uniform
@@ -1304,7 +1269,10 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     if (TCI_CHAIN_PROFILE) ph[5] += 1ull << 40;  // round count in the high bits
   }
 #undef TCI_PHASE
-#if TCI_CHAIN_PROFILE == 2  // per wave: barrier wait (slot w) and eval + prior + exchange (slot 4 + w)
+#if TCI_CHAIN_PROFILE == 3  // every phase of every wave: slot 8 w + k
+  if (lane == 0 && st.prof != nullptr)
+    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&st.prof[8 * w + k], (unsigned long long)ph[k]);
+#elif TCI_CHAIN_PROFILE == 2  // per wave: barrier wait (slot w) and eval + prior + exchange (slot 4 + w)
   if (lane == 0 && st.prof != nullptr) {
     atomicAdd((unsigned long long*)&st.prof[w], (unsigned long long)ph[3]);
     atomicAdd((unsigned long long*)&st.prof[4 + w], (unsigned long long)(ph[1] + ph[2]));
@@ -1315,8 +1283,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 #endif
   // the last round's rows
   if (w == kRecWave) {
-    store_vec();
-    acc_vec();
+    flush_vec();
 #pragma unroll
     for (int k = 0; k < NJ; ++k) {
       const int j = lane + 64 * k;
@@ -1328,7 +1295,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       st.naccept[c] = nacc;
       st.nrej_win[c] = nrej;
       st.nevals[c] = nev;
-      if (c == 0) *st.step = s_end;  // the adaptation reads the row it follows
+      if (c == st.c0) *st.step = s_end;  // the adaptation reads the row it follows
     }
     if (with_records) {  // the chunk ends a window (or the run): its records
       ca.finish(st, p, c, s_end, P, lane);
@@ -1346,9 +1313,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   }
   if (w == kSigWave) {
     const double x0 = (p.updatesigma && gpend) ? 1.0 / (Gl * (2.0 / ss)) : s2c;
-    store_s2();  // the previous round's rows
-    acc_s2(x0);
-    store_s2();  // the last round's rows
+    flush_s2(x0);
     if (lane == 0) {
       st.sigma2[c] = x0;
       if (with_records) {
@@ -1379,8 +1344,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   __shared__ double racc[NW][3][64 * NJ];  // each wave's window column sums ws, S1, S2 (ColAcc, in LDS)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int lane = threadIdx.x & 63;  // re-laundered every step (launder_lane)
-  const int64_t c = (int64_t)blockIdx.x * NW + w;
-  if (c >= st.n_chains) return;  // uniform per wave; no workgroup barriers below
+  const int64_t c = st.c0 + (int64_t)blockIdx.x * NW + w;
+  if (c >= st.c1) return;  // uniform per wave; no workgroup barriers below
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int64_t DW = draw_stride(ld);
@@ -1429,7 +1394,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     ra[64 * k + lane] = cont && in ? st.wsumv[c * ld + j] : 0.0;
     rb[64 * k + lane] = cont && in ? st.wacc1[c * ld + j] : 0.0;
     rc[64 * k + lane] = cont && in ? st.wacc2[c * ld + j] : 0.0;
-    ca.K[k] = !in ? 0.0 : !ca.kfirst ? st.smean[c * ld + j] : cont ? st.window[c * p.win * ld + j] : 0.0;
+    ca.K[k] = !in ? 0.0 : !ca.kfirst ? st.smean[c * ld + j]
+                                       : ca.sf < s_begin ? st.window[(c * p.win + log_slot(p, ca.sf)) * ld + j] : 0.0;
   }
   // ssfun and prior of the proposal th + scale * u (k_chain's per-wave evaluation); an in-bounds
   // proposal is left in yb (a move copies it from there)
@@ -1526,7 +1492,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
       const bool keep = st.chain_out != nullptr && kept_row(p, s, kk);
 #pragma unroll
       for (int k = 0; k < NJ; ++k) {
-        if (ca.kfirst && s == ca.first) ca.K[k] = th[k];
+        if (ca.kfirst && s == ca.sf) ca.K[k] = th[k];
         const int i = 64 * k + lane;
         ra[i] = ra[i] + th[k];
         if (s >= ca.sf) {
@@ -1589,12 +1555,13 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
   const int npass = draws_passes(p.walk != 0);
   const int64_t per_wg = (int64_t)kDrawSteps * npass;  // <= the workgroup's threads (scalar draws)
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
-  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(64 * 4), lds, stream, st, p, s_begin, s_end, npass);
+  const int64_t nc = st.c1 - st.c0;
+  hipLaunchKernelGGL(kd, dim3((unsigned)nc, gy), dim3(64 * 4), lds, stream, st, p, s_begin, s_end, npass);
   if (p.walk)
-    hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, stream, st, p,
+    hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((nc + 3) / 4)), dim3(kThreads), 0, stream, st, p,
                        kp, s_begin, s_end, with_records);
   else
-    hipLaunchKernelGGL((k_chain<RPL, NSEG, (RPL <= 2 ? kChainEPW : 1)>), dim3((unsigned)st.n_chains), dim3(kThreads), 0,
+    hipLaunchKernelGGL((k_chain<RPL, NSEG, (RPL <= 2 ? kChainEPW : 1)>), dim3((unsigned)nc), dim3(kThreads), 0,
                        stream, st, p, kp, s_begin, s_end, with_records);
   return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;
 }
@@ -1755,9 +1722,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int row = lane & 15, kq = lane >> 4;
-  const int64_t c = blockIdx.x;
+  const int64_t c = st.c0 + blockIdx.x;
   const int64_t step = *st.step;
-  if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
+  if (c >= st.c1 || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int NT = (P + 15) >> 4, LX = 16 * NT, T = NT * (NT + 1) / 2;
@@ -2042,9 +2009,9 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int row = lane & 15, kq = lane >> 4;
-  const int64_t c = blockIdx.x;
+  const int64_t c = st.c0 + blockIdx.x;
   const int64_t step = *st.step;
-  if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
+  if (c >= st.c1 || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int NT = (P + 15) >> 4, LX = 16 * NT, T = NT * (NT + 1) / 2;
@@ -2329,7 +2296,7 @@ int launch_adapt_mfma(const DramState& st, const DramParams& p, void* stream) {
   const size_t bytes = (size_t)adapt_mfma_lds_bytes(p.pmax);
   auto k = k_adapt_mfma<NW, MAXT, OWN, WPE>;
   if (ensure_dyn_lds((const void*)k, bytes) != TCI_OK) return TCI_EHIP;
-  hipLaunchKernelGGL(k, chain_grid(st.n_chains), dim3(64 * NW), bytes, (hipStream_t)stream, st, p);
+  hipLaunchKernelGGL(k, chain_grid(st.c1 - st.c0), dim3(64 * NW), bytes, (hipStream_t)stream, st, p);
   return finish();
 }
 
@@ -2360,7 +2327,7 @@ int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
   if (p.pmax <= 16 * 13) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
   const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax);
   if (ensure_dyn_lds((const void*)k_adapt_gt, lds) != TCI_OK) return TCI_EHIP;
-  hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.n_chains), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);
+  hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.c1 - st.c0), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);
   return finish();
 }
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,

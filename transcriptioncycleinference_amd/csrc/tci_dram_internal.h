@@ -17,6 +17,7 @@ constexpr int64_t dram_tri_stride(int64_t ld) { return (ld * (ld + 1) / 2 + 127)
 struct DramState {
   int64_t n_chains;
   int64_t ld;
+  int64_t c0, c1;          // the chains [c0, c1) a fused-engine launch works on (a chain group; 0, n_chains)
   const int32_t* cell;     // chain -> cell of the context
   const int64_t* key;      // chain -> RNG stream key (tci_dram_options.chain_keys; identity when absent)
   const int32_t* npar;     // P_c = 7 + N_c
@@ -63,7 +64,8 @@ struct DramState {
   double* chain_out;       // optional thinned chain rows (n_keep x n_chains x ld) or null
   double* s2_out;          // optional thinned s2 rows
   double* work;            // Cholesky tile grid of k_adapt_gt (n_chains x gt_lt(ld)^2)
-  int64_t* step;           // current chain row (1-based), advanced on device after each step
+  int64_t* step;           // current chain row (1-based), advanced on device after each step (one per chain
+                           // group: the fused engines may run groups of chains on their own streams)
   int64_t* prof;           // TCI_CHAIN_PROFILE builds only: k_chain phase cycles, summed over chains
   double* draws;           // fused engine: per chain, p.chunk rows of draw_stride(ld) doubles (k_draws)
 };
@@ -88,7 +90,7 @@ struct DramParams {
   int64_t pmax;        // max parameter count over the chains (picks the adaptation kernel)
   int64_t chunk;       // fused engine: rows per chain of the draws buffer (>= the longest chunk)
   int64_t walk;        // fused engine: 1 = one wavefront per chain walks the chunk (k_walk), 0 = k_chain
-  int64_t win;         // window rows per chain: adaptint, or (no adaptation) the fused engine's chunk; the
+  int64_t win;         // window rows per chain: adaptint, or (no adaptation) 100; the
                        // records are merged window by window (k_stats), the same partition for every engine
 };
 
