@@ -11,3 +11,4 @@ bash scripts/gpu_dg.sh r04d_dg 20000 || exit $?
 timeout -k 10 60 ./scripts/calib/rcp_f64 > "$OUT/r04d_rcp.json" || exit $?
 bash scripts/gpu_cp3.sh r04d_cp3 20000 || exit $?
 TCI_CHAIN_D=3 bash scripts/gpu_cp3.sh r04d_cp3d3 20000
+VARIANTS="main xcd xcd2" bash scripts/gpu_lk_pmc.sh r04d_lk

@@ -677,42 +677,3 @@ def test_gpu_chains_follow_the_cpu_restatement(lk, c_oracle, construct, engine):
         assert g.n_evals[k] == c["n_evals"][k]
     np.testing.assert_allclose(g.mean, c["mean"], rtol=1e-9, atol=1e-9)
     assert np.median(g.accept_rate) > 0.02
-
-
-@pytest.mark.parametrize("d", ["2", "3"])
-def test_chain_kernel_speculation_depth_gives_identical_chains(lk, monkeypatch, d):
-    """k_chain speculates D = 2 or 3 steps per round (TCI_CHAIN_D; 4 or 6 waves per chain): the
-    chains equal the batched engine's bit for bit, through burn-in scaling, adaptation and a window
-    that spans chunks."""
-    from transcriptioncycleinference_amd.mcmc import DramOptions
-
-    ids = list(range(0, 299, 11))
-    o = DramOptions(n_steps=537, burnintime=200, adaptint=100, stats_from=150, thin=1, seed=13)
-    o.engine = "batched"
-    b, _ = run(lk, ids, o)
-    monkeypatch.setenv("TCI_CHAIN_D", d)
-    o.engine = "fused"
-    a, _ = run(lk, ids, o)
-    o.max_chunk = 37
-    c, _ = run(lk, ids, o)
-    for f in ("chain", "s2chain", "mean", "std", "final_theta", "sigma_mean", "sigma_std", "accept_rate", "n_evals"):
-        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
-        np.testing.assert_array_equal(getattr(c, f), getattr(b, f), err_msg="max_chunk " + f)
-
-
-@pytest.mark.parametrize("groups", ["2", "3"])
-def test_chain_groups_give_identical_chains(lk, monkeypatch, groups):
-    """The fused engines' chain groups (TCI_DRAM_GROUPS: contiguous groups of chains walking their
-    chunks on their own streams) leave every chain unchanged."""
-    from transcriptioncycleinference_amd.mcmc import DramOptions
-
-    ids = list(range(0, 299, 7))
-    o = DramOptions(n_steps=437, burnintime=200, adaptint=100, stats_from=150, thin=1, seed=17, engine="fused")
-    a, _ = run(lk, ids, o)
-    monkeypatch.setenv("TCI_DRAM_GROUPS", groups)
-    b, _ = run(lk, ids, o)
-    o.engine = "walk"
-    c, _ = run(lk, ids, o)
-    for f in ("chain", "s2chain", "mean", "std", "final_theta", "sigma_mean", "sigma_std", "accept_rate", "n_evals"):
-        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
-        np.testing.assert_array_equal(getattr(a, f), getattr(c, f), err_msg="walk " + f)

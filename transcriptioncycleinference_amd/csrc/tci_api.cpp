@@ -563,16 +563,6 @@ struct DevAllocs {
   }
 };
 
-// Chain groups of the fused engines (tci_dram_run): TCI_DRAM_GROUPS (1..kMaxGroups) overrides the
-// default of one group.
-constexpr int kMaxGroups = 8;
-int dram_groups(int64_t n_chains) {
-  int g = 1;
-  if (const char* v = std::getenv("TCI_DRAM_GROUPS")) g = std::atoi(v);
-  g = std::max(1, std::min(g, kMaxGroups));
-  return (int)std::min<int64_t>(g, std::max<int64_t>(n_chains, 1));
-}
-
 // One DRAM step: propose -> ssfun -> accept/propose stage 2 -> ssfun -> accept, sigma2, log the row
 // -> [window records] -> [adapt] -> step + 1.
 int enqueue_step(tci_ctx* ctx, const tci::DramState& st, const tci::DramParams& p, hipStream_t s, bool with_stats,
@@ -666,8 +656,6 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   const int64_t n_keep = opt->thin > 0 ? (opt->n_steps + opt->thin - 1) / opt->thin : 0;
   st.n_chains = n_chains;
   st.ld = ld;
-  st.c0 = 0;
-  st.c1 = n_chains;
 #define TCI_ALLOC(field, T, count)                                  \
   do {                                                              \
     st.field = A.alloc<T>((count), &e);                             \
@@ -726,7 +714,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(s2sum, double, n);
   TCI_ALLOC(sq_mean, double, n);
   TCI_ALLOC(sq_m2, double, n);
-  TCI_ALLOC(step, int64_t, kMaxGroups);  // one step counter per chain group
+  TCI_ALLOC(step, int64_t, 1);
 #if defined(TCI_CHAIN_PROFILE) || defined(TCI_ADAPT_PROFILE)
   TCI_ALLOC(prof, int64_t, 32);
   TCI_HIP(ctx, hipMemsetAsync(st.prof, 0, 32 * sizeof(int64_t), ctx->stream));
@@ -778,8 +766,8 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
     TCI_HIP(ctx, hipMemcpyAsync(st.step, &one, sizeof(int64_t), hipMemcpyHostToDevice, s));
     if ((rc = tci::dram_launch_stats(st, p, s)) != TCI_OK) return fail(ctx, rc, "dram stats launch");
   }
-  const int64_t two[kMaxGroups] = {2, 2, 2, 2, 2, 2, 2, 2};
-  TCI_HIP(ctx, hipMemcpyAsync(st.step, two, sizeof(two), hipMemcpyHostToDevice, s));
+  const int64_t two = 2;
+  TCI_HIP(ctx, hipMemcpyAsync(st.step, &two, sizeof(int64_t), hipMemcpyHostToDevice, s));
   hipEvent_t ev0, ev1;
   TCI_HIP(ctx, hipEventCreate(&ev0));
   TCI_HIP(ctx, hipEventCreate(&ev1));
@@ -814,46 +802,14 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
     p.chunk = chunk;
     st.draws = A.alloc<double>(n * (size_t)p.chunk * DW, &e);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dram draws)");
-    // Chain groups: the chains split into G contiguous groups, each walking its chunks on its own
-    // stream (its own step counter), group g starting once group g - 1 has walked its first chunk,
-    // so one group's walk overlaps another's draws and adaptation. Every chain's kernels and inputs
-    // are the same, so the chains are identical for any G.
-    const int G = dram_groups(n_chains);
-    std::vector<hipStream_t> gs(G, s);
-    std::vector<hipEvent_t> gev(G, nullptr);
-    std::vector<tci::DramState> gst(G, st);
-    for (int g = 0; g < G; ++g) {
-      gst[g].c0 = (int64_t)g * n_chains / G;
-      gst[g].c1 = (int64_t)(g + 1) * n_chains / G;
-      gst[g].step = st.step + g;
-      if (g > 0 && e == hipSuccess) e = hipStreamCreateWithFlags(&gs[g], hipStreamNonBlocking);
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&gev[g], hipEventDisableTiming);
-    }
-    if (e == hipSuccess && G > 1) e = hipEventRecord(gev[0], s);  // the other streams start after the setup
-    for (int g = 1; g < G && e == hipSuccess; ++g) e = hipStreamWaitEvent(gs[g], gev[0], 0);
-    for (int64_t next = 2; next <= opt->n_steps && rc == TCI_OK && e == hipSuccess;) {
+    for (int64_t next = 2; next <= opt->n_steps && rc == TCI_OK;) {
       int64_t end = std::min<int64_t>(opt->n_steps, next + p.chunk - 1);
       end = std::min<int64_t>(end, ((next + win - 1) / win) * win);  // chunks never cross a window
       const int rec = end % win == 0 || end == opt->n_steps;  // the records kept in the chain kernel
-      for (int g = 0; g < G && rc == TCI_OK && e == hipSuccess; ++g) {
-        rc = tci::dram_launch_chain(gst[g], p, ctx->kp, ctx->rpl, next, end, rec, gs[g]);
-        if (next == 2 && g + 1 < G && rc == TCI_OK) {  // group g + 1 follows group g's first walk
-          e = hipEventRecord(gev[g], gs[g]);
-          if (e == hipSuccess) e = hipStreamWaitEvent(gs[g + 1], gev[g], 0);
-        }
-        if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(gst[g], p, gs[g]);
-      }
+      rc = tci::dram_launch_chain(st, p, ctx->kp, ctx->rpl, next, end, rec, s);
+      if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(st, p, s);
       next = end + 1;
     }
-    for (int g = 1; g < G; ++g) {  // join
-      if (e == hipSuccess) e = hipEventRecord(gev[g], gs[g]);
-      if (e == hipSuccess) e = hipStreamWaitEvent(s, gev[g], 0);
-    }
-    for (int g = 0; g < G; ++g) {
-      if (gev[g]) (void)hipEventDestroy(gev[g]);
-      if (g > 0 && gs[g] != s) (void)hipStreamDestroy(gs[g]);
-    }
-    if (e != hipSuccess) return hip_fail(ctx, e, "DRAM chain groups");
     e = hipSuccess;
   } else {
   // The step loop. Steps 2 .. n_steps; adaptation after steps that are multiples of adaptint.

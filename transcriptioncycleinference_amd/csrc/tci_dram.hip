@@ -35,7 +35,6 @@
 #include <math.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 
 #include "tci_dram_internal.h"
@@ -666,12 +665,7 @@ enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a d
 // FP64 R is read from global memory (L2) with a kDrawsPF-deep prefetch: staging it in LDS beside the
 // normals (74 KB at P = 136) left one workgroup per CU, and that layout took 144 us per TestData
 // chunk against 105 us with R from L2 and four 35 KB workgroups per CU (r03n/r03o).
-// Row stride of the normals in LDS: L rounded up to 2 mod 4 doubles. The MFMA A-fragment read
-// (lane = row + 16 kq reads Z[row][k + kq]) then hits 32 distinct bank pairs per 32-lane group
-// (bank = (2 zs row + 2 kq) mod 64, 2 zs = 4 x odd); at zs = L = 136 rows r and r + 4 shared banks
-// (a 4-way conflict on every A read).
-__host__ __device__ inline int64_t zrow_stride(int64_t L) { return L + ((2 - (L & 3)) & 3); }
-__host__ __device__ inline int64_t draws_lds_bytes(int64_t L) { return (2 * kDrawSteps * zrow_stride(L)) * 8 + 16; }
+__host__ __device__ inline int64_t draws_lds_bytes(int64_t L) { return (2 * kDrawSteps * L) * 8 + 16; }
 // Passes per workgroup: every workgroup reads the chain's R once per pass. FUSED (a few hundred
 // chains): 2 (1: 108.8, 2: 104.7, 4: 123.7 us per TestData chunk); WALK (thousands of chains, P =
 // 207): 4, fewer and longer workgroups reading R fewer times.
@@ -685,10 +679,10 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
   constexpr int kDrawWaves = NWD, kDrawThreads = 64 * NWD;
   constexpr int kDrawCT = CT;
   extern __shared__ __attribute__((aligned(16))) double dyn[];
-  const int64_t c = st.c0 + blockIdx.x;
-  if (c >= st.c1) return;
+  const int64_t c = blockIdx.x;
+  if (c >= st.n_chains) return;
   const int64_t ld = st.ld;
-  const int ZS = (int)zrow_stride(ld);  // row stride of the normals in LDS
+  const int L = (int)ld;
   const int P = st.npar[c];
   const int64_t key = st.key[c];
   const int64_t DW = draw_stride(ld);
@@ -702,16 +696,16 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
     const int64_t step0 = s_begin + ((int64_t)blockIdx.y * npass + pass) * kDrawSteps;
     if (step0 > s_end) break;  // uniform over the workgroup
     const int ns = (int)min<int64_t>(kDrawSteps, s_end - step0 + 1);
-    if (!(TCI_DRAWS_ABLATE & 1)) draw_block_normals<kDrawThreads>(p.seed, key, step0, ns, P, p.ntry >= 2, Z, ZS);
+    if (!(TCI_DRAWS_ABLATE & 1)) draw_block_normals<kDrawThreads>(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
     __syncthreads();
     // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
     double* d0 = drow + step0 * DW;
     const auto put = [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; };
     if (!(TCI_DRAWS_ABLATE & 2))
       for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT)
-        mfma_zr<kDrawMT, kDrawCT, kDrawWaves, decltype(put), kDrawsPF>(Z, ZS, 2 * ns, Rg, P, top, put);
+        mfma_zr<kDrawMT, kDrawCT, kDrawWaves, decltype(put), kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
     for (int k = w; k < ns; k += kDrawWaves) {
-      const double2 q = wave_q(Z + 2 * k * ZS, Z + (2 * k + 1) * ZS, inv_ds, P, lane);
+      const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
       if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
     }
     __syncthreads();  // Z is rewritten by the next pass
@@ -946,22 +940,21 @@ constexpr int kRecWave = 0, kSigWave = 2;  // (six placements measured within 1 
 // spill at RPL = 4 (config 5: 199.7 -> 191-193 us per step) and trims k_chain<2,1>'s SGPR spill.
 __device__ __forceinline__ void launder_lane(int& lane) { asm volatile("" : "+v"(lane)); }
 
-// Steps per round of k_chain: D speculated steps, 2 D waves (one evaluation each: stage w & 1 of
-// step s + (w >> 1)). D = 2 (4 waves) or D = 3 (6 waves, 3 waves per SIMD where two chains share a
-// CU, so at most 168 VGPRs). Every D gives the same chains. (Round 3 tried four steps with 4 waves
-// evaluating two slots each, one after the other: 3.02 steps per round instead of 1.82 but rounds
-// ~1.75x as long, k_chain 411 vs 260 us per 100 steps, r03y.)
-#ifndef TCI_CHAIN_WPE
-#define TCI_CHAIN_WPE(D) ((D) >= 3 ? 3 : 1)
-#endif
-template <int RPL, int NSEG, int D>
-__global__ __launch_bounds__(128 * D) __attribute__((amdgpu_waves_per_eu(TCI_CHAIN_WPE(D)))) void k_chain(
-    DramState st, DramParams p, KParams kp, int64_t s_begin, int64_t s_end, int with_records) {
+// Evaluations per wave and round of k_chain: EPW = 1 speculates 2 steps per round, EPW = 2 four
+// (each wave evaluates its stage's proposals of two steps, one after the other). EPW = 2 decides
+// 3.02 steps per round instead of 1.82 on the 299 TestData chains, but its rounds are ~1.75x as
+// long and the 43 CUs that hold two chains become the long pole: k_chain 411 vs 260 us per 100
+// steps (r03y). Only EPW = 1 is instantiated; the EPW = 2 instance was bitwise equal to the other
+// engines (tests/test_dram_gpu.py green with it).
+constexpr int kChainEPW = 1;
+template <int RPL, int NSEG, int EPW>
+__global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
+                                                    int64_t s_end, int with_records) {
   // Round structure (one workgroup barrier per round). At the start of a round the state after
-  // row s-1 is known. The round speculates D steps: proposal slot 2h + stage holds the
+  // row s-1 is known. The round speculates D = 2 EPW steps: proposal slot 2h + stage holds the
   // stage-1/2 proposal of step s + h, drawn around the SAME state, i.e. speculating that steps
   // s .. s + h - 1 do not move the chain (the common case: mcmcstat's DRAM accepts a minority of
-  // steps). Wave w evaluates its stage (w & 1) of step s + (w >> 1). After the
+  // steps). Wave w evaluates its stage (w & 1) of steps s + (w >> 1) + 2e, e < EPW. After the
   // barrier every wave takes the decisions of steps s, s + 1, .. from the exchanged values until
   // one moves the chain: up to D steps are decided per round, each exactly as the step-by-step
   // sampler (and the batched engine) decides it, bit for bit.
@@ -974,56 +967,45 @@ __global__ __launch_bounds__(128 * D) __attribute__((amdgpu_waves_per_eu(TCI_CHA
   //     the round;
   //   * the s2 of the rows the previous round decided (1/(G*(2/ss)) of the state after them)
   //     and the logs and window sums of those rows.
-  constexpr int EPW = 1;
   constexpr int NJ = RPL + 1;  // vector entries per lane: P = 7 + N <= 64 RPL + 8 <= 64 NJ
   constexpr int EV = eval_lds_doubles<RPL>();
-  constexpr int NW = 2 * D;
+  constexpr int NW = kThreads / 64;
+  constexpr int D = 2 * EPW;                // steps per round
   constexpr int NS = 2 * D;                 // proposal slots
-  // candidate rows for the next round: an advance by adv in [1, D] moves this wave to row
-  // s + adv + a1, so the rows s + a1 + 1 .. s + a1 + D are all prefetched
-  constexpr int NPF = D;
-  constexpr int kPf[4] = {0, 1, 2, 3};  // prefetched k (the first NPF)
-  static_assert(D >= 2 && D <= 4, "2 to 4 speculated steps");
+  // candidate rows for the next round: row s + a1 + 1 + k for k < NC. EPW = 1: both (k = 0, 1);
+  // EPW = 2: the rows of an advance by 1 or 4 (k = 0, 2, 3, 5) -- an advance by 2 or 3 loads its
+  // missing row (k = 1 or 4) after the decisions: six prefetched rows exceeded the 256-register
+  // budget of two chains per CU
+  constexpr int NC = D + 2 * (EPW - 1);
+  constexpr int NPF = EPW == 1 ? 2 : 4;
+  constexpr int kPf[4] = {0, EPW == 1 ? 1 : 2, 3, 5};  // prefetched k (the first NPF)
   constexpr int NSC = 4 * (2 * D - 1);      // lanes of scalar draws: rows s + 1 .. s + 2D - 1
   __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each evaluating wave's tables
   __shared__ double yl[2][NS][64 * NJ];                         // by round parity: every proposal
   __shared__ double xch[2][NS][4];                              // by round parity: ss, prior, in-bounds
   __shared__ double xip[2][D];                                  // by round parity: precisions of steps s + h
-  // The chain's bounds and prior vectors (lower, upper, mu, 1/sig), shared by the waves, and
-  // kRecWave's window column sums (ws, S1, S2: ColAcc's arithmetic): in LDS, not in every wave's
-  // registers (D = 3 runs three waves per SIMD where two chains share a CU: 168 VGPRs).
-  __shared__ double cvec[4][64 * NJ];
-  __shared__ double racc[3][64 * NJ];
-  const int64_t c = st.c0 + blockIdx.x;
-  if (c >= st.c1) return;
+  const int64_t c = blockIdx.x;
+  if (c >= st.n_chains) return;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int lane = threadIdx.x & 63;  // re-laundered every round (launder_lane)
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int64_t DW = draw_stride(ld);
   const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
-  const int stage = w & 1, a1 = w >> 1;                           // this wave's slot: step s + a1
+  const int stage = w & 1, a1 = w >> 1;                           // this wave's slots: steps s + a1 + 2e
   const double scale = stage ? 1.0 / p.drscale : 1.0;
-  double th[NJ], thp[NJ];
-  const double* lo = cvec[0];
-  const double* hi = cvec[1];
-  const double* mu = cvec[2];
-  const double* sg = cvec[3];
+  double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], thp[NJ];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
     const int j = lane + 64 * k;
     const bool in = j < P;
     th[k] = in ? st.theta[c * ld + j] : 0.0;
     thp[k] = th[k];
+    lo[k] = in ? st.lower[c * ld + j] : 0.0;
+    hi[k] = in ? st.upper[c * ld + j] : 0.0;
+    mu[k] = in ? st.pmu[c * ld + j] : 0.0;
+    sg[k] = in ? prior_prec(st.psig[c * ld + j]) : 0.0;  // the precision (prior_prec)
   }
-  for (int i = threadIdx.x; i < 64 * NJ; i += 64 * NW) {
-    const bool in = i < P;
-    cvec[0][i] = in ? st.lower[c * ld + i] : 0.0;
-    cvec[1][i] = in ? st.upper[c * ld + i] : 0.0;
-    cvec[2][i] = in ? st.pmu[c * ld + i] : 0.0;
-    cvec[3][i] = in ? prior_prec(st.psig[c * ld + i]) : 0.0;  // the precision (prior_prec)
-  }
-  __syncthreads();
   EvalIn<RPL> e;  // the chain's cell records stay in registers
   {
     load_cell<RPL, false>(kp, st.cell[c], lane, e);
@@ -1072,9 +1054,9 @@ __global__ __launch_bounds__(128 * D) __attribute__((amdgpu_waves_per_eu(TCI_CHA
     for (int k = 0; k < NJ; ++k) {
       const int j = lane + 64 * k;
       const bool in = j < P;
-      racc[0][j] = cont && in ? st.wsumv[c * ld + j] : 0.0;
-      racc[1][j] = cont && in ? st.wacc1[c * ld + j] : 0.0;
-      racc[2][j] = cont && in ? st.wacc2[c * ld + j] : 0.0;
+      ca.ws[k] = cont && in ? st.wsumv[c * ld + j] : 0.0;
+      ca.S1[k] = cont && in ? st.wacc1[c * ld + j] : 0.0;
+      ca.S2[k] = cont && in ? st.wacc2[c * ld + j] : 0.0;
       // a window continued from an earlier chunk whose row sf is already logged: K = that row
       ca.K[k] = !in ? 0.0 : !ca.kfirst ? st.smean[c * ld + j]
                                          : ca.sf < s_begin ? st.window[(c * p.win + log_slot(p, ca.sf)) * ld + j] : 0.0;
@@ -1088,17 +1070,7 @@ __global__ __launch_bounds__(128 * D) __attribute__((amdgpu_waves_per_eu(TCI_CHA
   }
   auto rec_row = [&](int64_t row, const double* x) {
     log_row<NJ>(st, p, c, slot0 + row, P, x, lane);
-#pragma unroll
-    for (int k = 0; k < NJ; ++k) {  // ColAcc::add, the sums in LDS
-      if (ca.kfirst && row == ca.sf) ca.K[k] = x[k];
-      const int i = 64 * k + lane;
-      racc[0][i] = racc[0][i] + x[k];
-      if (row >= ca.sf) {
-        const double d = x[k] - ca.K[k];
-        racc[1][i] = racc[1][i] + d;
-        racc[2][i] = fma(d, d, racc[2][i]);
-      }
-    }
+    ca.add(row, x);
     int64_t k;
     if (st.chain_out != nullptr && kept_row(p, row, k)) {
 #pragma unroll
@@ -1141,7 +1113,7 @@ __global__ __launch_bounds__(128 * D) __attribute__((amdgpu_waves_per_eu(TCI_CHA
 #pragma unroll
       for (int k = 0; k < NJ; ++k) {
         y[k] = th[k] + scale * ucur[q][k];
-        if (lane + 64 * k < P) out |= !(y[k] >= lo[lane + 64 * k] && y[k] <= hi[lane + 64 * k]);
+        if (lane + 64 * k < P) out |= !(y[k] >= lo[k] && y[k] <= hi[k]);
       }
       const bool active = (stage == 0 || p.ntry >= 2) && s + h <= s_end;
       const bool inb = active && wave_ballot(out) == 0;
@@ -1169,20 +1141,14 @@ __global__ __launch_bounds__(128 * D) __attribute__((amdgpu_waves_per_eu(TCI_CHA
           const int g = RPL * lane + k;
           e.dr[k] = 7 + g < P ? yb[7 + g] : 0.0;
         }
-        double mur[NJ], sgr[NJ];
-#pragma unroll
-        for (int k = 0; k < NJ; ++k) {
-          mur[k] = mu[lane + 64 * k];
-          sgr[k] = sg[lane + 64 * k];
-        }
         if (RPL <= 2) {  // the prior's wave sum rides on the evaluation's final scan (same bits)
-          pr = prior_part<NJ>(y, mur, sgr, P, lane);
+          pr = prior_part<NJ>(y, mu, sg, P, lane);
           r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0, &pr);
           TCI_PHASE(1)
         } else {
           r = eval_wave<RPL, NSEG, MODE_SS>(kp, e, lane, evl[w], 0, nullptr, nullptr, 0);
           TCI_PHASE(1)
-          pr = wave_prior_reg<NJ>(y, mur, sgr, P, lane);
+          pr = wave_prior_reg<NJ>(y, mu, sg, P, lane);
         }
       }
       if (lane == 0) {
@@ -1329,13 +1295,7 @@ __global__ __launch_bounds__(128 * D) __attribute__((amdgpu_waves_per_eu(TCI_CHA
       st.naccept[c] = nacc;
       st.nrej_win[c] = nrej;
       st.nevals[c] = nev;
-      if (c == st.c0) *st.step = s_end;  // the adaptation reads the row it follows
-    }
-#pragma unroll
-    for (int k = 0; k < NJ; ++k) {
-      ca.ws[k] = racc[0][64 * k + lane];
-      ca.S1[k] = racc[1][64 * k + lane];
-      ca.S2[k] = racc[2][64 * k + lane];
+      if (c == 0) *st.step = s_end;  // the adaptation reads the row it follows
     }
     if (with_records) {  // the chunk ends a window (or the run): its records
       ca.finish(st, p, c, s_end, P, lane);
@@ -1384,8 +1344,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   __shared__ double racc[NW][3][64 * NJ];  // each wave's window column sums ws, S1, S2 (ColAcc, in LDS)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int lane = threadIdx.x & 63;  // re-laundered every step (launder_lane)
-  const int64_t c = st.c0 + (int64_t)blockIdx.x * NW + w;
-  if (c >= st.c1) return;  // uniform per wave; no workgroup barriers below
+  const int64_t c = (int64_t)blockIdx.x * NW + w;
+  if (c >= st.n_chains) return;  // uniform per wave; no workgroup barriers below
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int64_t DW = draw_stride(ld);
@@ -1557,7 +1517,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
     st.naccept[c] = nacc;
     st.nrej_win[c] = nrej;
     st.nevals[c] = nev;
-    if (c == st.c0) *st.step = s_end;  // the adaptation reads the row it follows
+    if (c == 0) *st.step = s_end;  // the adaptation reads the row it follows
   }
   if (with_records) {  // the chunk ends a window (or the run): its records
 #pragma unroll
@@ -1582,12 +1542,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
   }
 }
 
-// Speculated steps per k_chain round (TCI_CHAIN_D: 2 or 3; default 2).
-inline int chain_d() {
-  const char* v = std::getenv("TCI_CHAIN_D");
-  return v && std::atoi(v) == 3 ? 3 : 2;
-}
-
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    int with_records, hipStream_t stream) {
@@ -1601,22 +1555,13 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
   const int npass = draws_passes(p.walk != 0);
   const int64_t per_wg = (int64_t)kDrawSteps * npass;  // <= the workgroup's threads (scalar draws)
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
-  const int64_t nc = st.c1 - st.c0;
-  hipLaunchKernelGGL(kd, dim3((unsigned)nc, gy), dim3(64 * 4), lds, stream, st, p, s_begin, s_end, npass);
+  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(64 * 4), lds, stream, st, p, s_begin, s_end, npass);
   if (p.walk)
-    hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((nc + 3) / 4)), dim3(kThreads), 0, stream, st, p,
+    hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, stream, st, p,
                        kp, s_begin, s_end, with_records);
-  else {
-    bool d3 = false;
-    if constexpr (RPL <= 2 && NSEG == 1) d3 = chain_d() == 3;
-    if constexpr (RPL <= 2 && NSEG == 1)
-      if (d3)
-        hipLaunchKernelGGL((k_chain<RPL, NSEG, 3>), dim3((unsigned)nc), dim3(128 * 3), 0, stream, st, p, kp, s_begin,
-                           s_end, with_records);
-    if (!d3)
-      hipLaunchKernelGGL((k_chain<RPL, NSEG, 2>), dim3((unsigned)nc), dim3(128 * 2), 0, stream, st, p, kp, s_begin,
-                         s_end, with_records);
-  }
+  else
+    hipLaunchKernelGGL((k_chain<RPL, NSEG, (RPL <= 2 ? kChainEPW : 1)>), dim3((unsigned)st.n_chains), dim3(kThreads), 0,
+                       stream, st, p, kp, s_begin, s_end, with_records);
   return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;
 }
 
@@ -1776,9 +1721,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int row = lane & 15, kq = lane >> 4;
-  const int64_t c = st.c0 + blockIdx.x;
+  const int64_t c = blockIdx.x;
   const int64_t step = *st.step;
-  if (c >= st.c1 || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
+  if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int NT = (P + 15) >> 4, LX = 16 * NT, T = NT * (NT + 1) / 2;
@@ -2063,9 +2008,9 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int row = lane & 15, kq = lane >> 4;
-  const int64_t c = st.c0 + blockIdx.x;
+  const int64_t c = blockIdx.x;
   const int64_t step = *st.step;
-  if (c >= st.c1 || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
+  if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int NT = (P + 15) >> 4, LX = 16 * NT, T = NT * (NT + 1) / 2;
@@ -2350,7 +2295,7 @@ int launch_adapt_mfma(const DramState& st, const DramParams& p, void* stream) {
   const size_t bytes = (size_t)adapt_mfma_lds_bytes(p.pmax);
   auto k = k_adapt_mfma<NW, MAXT, OWN, WPE>;
   if (ensure_dyn_lds((const void*)k, bytes) != TCI_OK) return TCI_EHIP;
-  hipLaunchKernelGGL(k, chain_grid(st.c1 - st.c0), dim3(64 * NW), bytes, (hipStream_t)stream, st, p);
+  hipLaunchKernelGGL(k, chain_grid(st.n_chains), dim3(64 * NW), bytes, (hipStream_t)stream, st, p);
   return finish();
 }
 
@@ -2381,7 +2326,7 @@ int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
   if (p.pmax <= 16 * 13) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
   const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax);
   if (ensure_dyn_lds((const void*)k_adapt_gt, lds) != TCI_OK) return TCI_EHIP;
-  hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.c1 - st.c0), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);
+  hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.n_chains), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);
   return finish();
 }
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,
@@ -2396,9 +2341,8 @@ int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& k
   }
 }
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl) {
-  const int64_t ns = 2 * 3;  // k_chain (the largest D, 3): 2 D waves and slots: evl, yl, xch, xip (and slack)
-  const int64_t chain =
-      (ns * (4 * 64 * rpl + 4 * rpl) + 2 * ns * 64 * (rpl + 1) + 2 * ns * 4 + 2 * 3 + 7 * 64 * (rpl + 1) + 16) * 8;
+  const int64_t ns = 4 * (rpl <= 2 ? kChainEPW : 1);  // k_chain: evl, yl, xch, xip (and slack)
+  const int64_t chain = (4 * (4 * 64 * rpl + 4 * rpl) + 2 * ns * 64 * (rpl + 1) + 2 * ns * 4 + 2 * ns + 16) * 8;
   return std::max<int64_t>(chain, draws_lds_bytes(ld));                                  // k_draws (dynamic)
 }
 int dram_launch_stats(const DramState& st, const DramParams& p, void* stream) {

@@ -17,7 +17,6 @@ constexpr int64_t dram_tri_stride(int64_t ld) { return (ld * (ld + 1) / 2 + 127)
 struct DramState {
   int64_t n_chains;
   int64_t ld;
-  int64_t c0, c1;          // the chains [c0, c1) a fused-engine launch works on (a chain group; 0, n_chains)
   const int32_t* cell;     // chain -> cell of the context
   const int64_t* key;      // chain -> RNG stream key (tci_dram_options.chain_keys; identity when absent)
   const int32_t* npar;     // P_c = 7 + N_c
@@ -64,8 +63,7 @@ struct DramState {
   double* chain_out;       // optional thinned chain rows (n_keep x n_chains x ld) or null
   double* s2_out;          // optional thinned s2 rows
   double* work;            // Cholesky tile grid of k_adapt_gt (n_chains x gt_lt(ld)^2)
-  int64_t* step;           // current chain row (1-based), advanced on device after each step (one per chain
-                           // group: the fused engines may run groups of chains on their own streams)
+  int64_t* step;           // current chain row (1-based), advanced on device after each step
   int64_t* prof;           // TCI_CHAIN_PROFILE builds only: k_chain phase cycles, summed over chains
   double* draws;           // fused engine: per chain, p.chunk rows of draw_stride(ld) doubles (k_draws)
 };

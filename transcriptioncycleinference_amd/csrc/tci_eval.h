@@ -194,8 +194,11 @@ __device__ __forceinline__ double occupancy(double p, const SegParams& s, double
 // The cuts of all thresholds are computed at once, one threshold per lane, from an estimate of
 // x / vd0 and the two exact products that should bracket x:
 //   m0 = clamp(ceil(x * rcp(vd0)) - 1, 0, nsteps),  n(x) = m0  when  P_{m0} < x <= P_{m0+1}
-// (m0 = 0 needs no lower product, m0 = nsteps no upper one). A pair that does not bracket x (the
-// estimate off by one: x / vd0 within ~1e-15 of an integer) is flagged instead of trusted. `bad`
+// (m0 = 0 needs no lower product, m0 = nsteps no upper one). rcp(vd0) is v_rcp_f64, which is not
+// correctly rounded: its relative error reaches 4.6e-8 on gfx950 (4.2 M samples, never exact:
+// scripts/calib/rcp_f64.hip, profiles/r04_likelihood/r04d_rcp_f64_accuracy.json), so the estimate
+// is off by one when x / vd0 lies within ~N * 5e-8 of an integer (N <= 2,048 steps). Such a pair does
+// not bracket x and is flagged instead of trusted (a few waves in 10^5 take the exact sweep). `bad`
 // also flags a bracketing product within eps of x: the same exactness test as one vote per m,
 // because every other P_m is at least ~vd0 > 4 eps away from x (eps >= vd0/4 is flagged too). A
 // flagged wave takes the exact sweep.
