@@ -991,7 +991,12 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int64_t DW = draw_stride(ld);
-  const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
+  // this chain's draws rows (row of step s at (s - s_begin) * DW) and window logs (slot r at r * ld):
+  // 32-bit offsets from per-chain bases (a chunk is <= 1,000 rows), no 64-bit multiplies in the loop
+  const double* const dchain = st.draws + c * p.chunk * DW;
+  double* const wlog = st.window + c * p.win * ld;
+  double* const s2lg = st.s2log + c * p.win;
+  const int DWi = (int)DW, ldi = (int)ld;
   const int stage = w & 1, a1 = w >> 1;                           // this wave's slots: steps s + a1 + 2e
   const double scale = stage ? 1.0 / p.drscale : 1.0;
   double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ], thp[NJ];
@@ -1027,13 +1032,17 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   // draws of rows s + 1 .. s + 2D - 1) and the next round picks its rows: a whole round hides the
   // latency. The scalar draws are vector loads (lane j: row r0 + j / 4, slot j % 4) read by
   // readlane: scalar loads would also be waited for at the evaluation's first LDS wait.
+  // Unconditional loads (indices clamped into the row: no exec-mask branches), zeros selected past P.
   auto load_u = [&](double* u, int64_t row) {
-    const double* src = drow + min(row, s_end) * DW + stage * ld;
+    const double* src = dchain + (int)(min(row, s_end) - s_begin) * DWi + stage * ldi;
 #pragma unroll
-    for (int k = 0; k < NJ; ++k) u[k] = lane + 64 * k < P ? src[lane + 64 * k] : 0.0;
+    for (int k = 0; k < NJ; ++k) {
+      const double v = src[min(lane + 64 * k, P - 1)];
+      u[k] = lane + 64 * k < P ? v : 0.0;
+    }
   };
-  auto load_sc = [&](int64_t r0) {
-    return lane < NSC ? drow[min(r0 + (lane >> 2), s_end) * DW + 2 * ld + (lane & 3)] : 0.0;
+  auto load_sc = [&](int64_t r0) {  // lanes >= NSC load a valid entry that is never read
+    return dchain[(int)(min(r0 + (lane >> 2), s_end) - s_begin) * DWi + 2 * ldi + (lane & 3)];
   };
   double ucur[EPW][NJ], cand[NPF][NJ];
 #pragma unroll
@@ -1068,21 +1077,35 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     qa.S2 = cont ? st.s2acc[3 * c + 2] : 0.0;
     qa.K = ca.first > 1 ? st.sq_mean[c] : sqrt(st.s2log[c * p.win]);
   }
-  auto rec_row = [&](int64_t row, const double* x) {
-    log_row<NJ>(st, p, c, slot0 + row, P, x, lane);
-    ca.add(row, x);
-    int64_t k;
-    if (st.chain_out != nullptr && kept_row(p, row, k)) {
+  // thinned output rows: the next kept row >= s_begin and its index, advanced as rows are recorded
+  // (no division per row); never matched when nothing is kept
+  const bool keep_rows = (st.chain_out != nullptr || st.s2_out != nullptr) && p.thin > 0;
+  int64_t kkeep = keep_rows ? (s_begin - 1 + p.thin - 1) / p.thin : 0;
+  int64_t next_keep = keep_rows ? kkeep * p.thin + 1 : INT64_MAX;
+  auto rec_row = [&](int64_t row, const double* x) {  // kRecWave
+    double* wr = wlog + (int)(slot0 + row) * ldi;
 #pragma unroll
-      for (int q = 0; q < NJ; ++q)
-        if (lane + 64 * q < P) st.chain_out[(k * st.n_chains + c) * ld + lane + 64 * q] = x[q];
+    for (int k = 0; k < NJ; ++k)
+      if (lane + 64 * k < P) wr[lane + 64 * k] = x[k];
+    ca.add(row, x);
+    if (row == next_keep) {  // uniform
+      if (st.chain_out != nullptr && kkeep < p.n_keep) {
+#pragma unroll
+        for (int q = 0; q < NJ; ++q)
+          if (lane + 64 * q < P) st.chain_out[(kkeep * st.n_chains + c) * ld + lane + 64 * q] = x[q];
+      }
+      ++kkeep;
+      next_keep += p.thin;
     }
   };
-  auto rec_s2 = [&](int64_t row, double v) {  // lane 0
-    log_s2(st, p, c, slot0 + row, v);
-    qa.add(v);
-    int64_t k;
-    if (st.s2_out != nullptr && kept_row(p, row, k)) st.s2_out[k * st.n_chains + c] = v;
+  auto rec_s2 = [&](int64_t row, double v) {  // kSigWave: the row bookkeeping in every lane, stores by lane 0
+    if (lane == 0) s2lg[(int)(slot0 + row)] = v;
+    if (lane == 0) qa.add(v);
+    if (row == next_keep) {  // uniform
+      if (lane == 0 && st.s2_out != nullptr && kkeep < p.n_keep) st.s2_out[kkeep * st.n_chains + c] = v;
+      ++kkeep;
+      next_keep += p.thin;
+    }
   };
   auto flush_vec = [&]() {  // unrolled: a bounded store count (a runtime loop made the compiler
                             // wait for every store before the next round's loads were used)
@@ -1092,12 +1115,10 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     if (padv >= 1) rec_row(prow + padv - 1, th);
   };
   auto flush_s2 = [&](double x0) {
-    if (lane == 0) {
 #pragma unroll
-      for (int i = 0; i < D - 1; ++i)
-        if (i + 1 < padv) rec_s2(prow + i, s2f[i]);
-      if (padv >= 1) rec_s2(prow + padv - 1, x0);
-    }
+    for (int i = 0; i < D - 1; ++i)
+      if (i + 1 < padv) rec_s2(prow + i, s2f[i]);  // uniform
+    if (padv >= 1) rec_s2(prow + padv - 1, x0);
   };
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = stamp(), t1;
 #define TCI_PHASE(k) \
@@ -1109,14 +1130,14 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     for (int q = 0; q < EPW; ++q) {
       const int h = a1 + 2 * q;  // step s + h
       double y[NJ];
-      bool out = false;
+      uint64_t outm = 0;  // lanes with an entry outside its bounds: votes on the compare masks, no branches
 #pragma unroll
       for (int k = 0; k < NJ; ++k) {
         y[k] = th[k] + scale * ucur[q][k];
-        if (lane + 64 * k < P) out |= !(y[k] >= lo[k] && y[k] <= hi[k]);
+        outm |= (wave_ballot(!(y[k] >= lo[k])) | wave_ballot(!(y[k] <= hi[k]))) & wave_ballot(lane + 64 * k < P);
       }
       const bool active = (stage == 0 || p.ntry >= 2) && s + h <= s_end;
-      const bool inb = active && wave_ballot(out) == 0;
+      const bool inb = active && outm == 0;
       if (q == 0) {  // the next round's candidates (see load_u)
 #pragma unroll
         for (int k = 0; k < NPF; ++k) load_u(cand[k], s + a1 + 1 + kPf[k]);
