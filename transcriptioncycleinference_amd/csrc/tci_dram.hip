@@ -122,7 +122,8 @@ __device__ __forceinline__ double uniform_at(uint64_t seed, int64_t c, int64_t s
 // variate is (d*v)*scale. The unit variate depends only on the stream and a, so the fused engine
 // draws it ahead of the chain (k_draws) and the scale (2/SS of the current state) is applied when
 // it is used: the same bits as gamma_at.
-__device__ double gamma_unit(uint64_t seed, int64_t c, int64_t step, double a) {
+template <int = 0>  // the body, inlined where the caller's register budget needs it (k_draws)
+__device__ __forceinline__ double gamma_unit_t(uint64_t seed, int64_t c, int64_t step, double a) {
   const double d = a - 1.0 / 3.0, cc = 1.0 / sqrt(9.0 * d);
   for (uint32_t it = 0; it < 1024; ++it) {
     const uint4 r = rng(seed, c, step, P_GAMMA, it);
@@ -139,6 +140,7 @@ __device__ double gamma_unit(uint64_t seed, int64_t c, int64_t step, double a) {
   }
   return a;  // unreachable in practice (acceptance > 0.95 per try)
 }
+__device__ double gamma_unit(uint64_t seed, int64_t c, int64_t step, double a) { return gamma_unit_t(seed, c, step, a); }
 __device__ __forceinline__ double gamma_at(uint64_t seed, int64_t c, int64_t step, double a, double scale) {
   return gamma_unit(seed, c, step, a) * scale;
 }
@@ -331,6 +333,87 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const do
         const double b = (i <= j && j < P) ? rv : 0.0;
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[g][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b, acc[g][m], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < CT; ++g) {
+    const int j = 16 * nt[g] + row;
+    if (kmx[g] < 0 || j >= P) continue;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * m + kq + 4 * q;
+        if (r < M) store(r, j, acc[g][m][q]);
+      }
+  }
+}
+// k_draws' z*R with R in global memory (L2): mfma_zr's tiles, products and k order (the same
+// bits) as a software pipeline. The R values of k-step i0 + 4 PF are loaded while k-step i0 runs,
+// into a ring of PF register sets (no copies, so each load has PF k-steps to land); Z is read
+// without exec-mask branches (rows past M read row M - 1, whose products are never stored; k past
+// P reads finite LDS -- the zero-filled pads or the next row's normals -- and meets a zero R entry);
+// the packed-R row offset advances by one addition per k-step. Phases run whole rings: the extra
+// k-steps past a tile's last row multiply zero R entries and leave its accumulators' bits as they
+// are (accumulators start at +0, products of finite values with 0 are +-0).
+template <int MT, int CT, int NWV, int PF, class Store>
+__device__ __forceinline__ void mfma_zr_pf(const double* Z, int zs, int M, const double* __restrict__ Rg, int P,
+                                           int top, Store store) {
+  static_assert(PF >= 1 && PF <= 2, "reads reach k = P + 4 PF - 2: draws_lds_bytes pads 8 doubles");
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int row = lane & 15, kq = lane >> 4;
+  int nt[CT], kmx[CT], jv[CT], jc[CT];
+#pragma unroll
+  for (int g = 0; g < CT; ++g) {
+    nt[g] = top - (NWV * g + ((g & 1) ? NWV - 1 - w : w));  // uniform: costliest first, snake order
+    kmx[g] = nt[g] >= 0 ? min(16 * nt[g] + 15, P - 1) : -1;
+    const int j = 16 * nt[g] + row;
+    jv[g] = j < P ? j : -1;  // R row i contributes to column j while i <= jv (never past P)
+    jc[g] = min(max(j, 0), P - 1);
+  }
+  // this lane's A entries at k-step 0 (k = kq)
+  int za[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) za[m] = min(16 * m + row, M - 1) * zs + kq;
+  // f(i) = tri_off(i, P) - i = i (2P - 1 - i) / 2: entry (i, j) of the packed R at f(i) + j. f rises
+  // to i = P - 1, f(P) = f(P - 1), then falls (below 0 past 2P - 1), so max(f, 0) + j stays inside
+  // [0, P(P+1)/2) for the loads past a tile's rows (their values are never used). f(i + 4) = f(i) +
+  // 4P - 10 - 4i.
+  int fl = kq * (P - 1) - (kq * (kq - 1)) / 2;  // f(il + kq) for the next load's k-step il
+  int il = 0;
+  auto load_next = [&](double* b) {
+#pragma unroll
+    for (int g = 0; g < CT; ++g) b[g] = Rg[max(fl, 0) + jc[g]];
+    fl += 4 * P - 10 - 4 * il - 4 * kq;
+    il += 4;
+  };
+  f64x4 acc[CT][MT];
+#pragma unroll
+  for (int g = 0; g < CT; ++g)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[g][m] = f64x4{0.0, 0.0, 0.0, 0.0};
+  double bq[PF][CT];
+#pragma unroll
+  for (int d = 0; d < PF; ++d) load_next(bq[d]);
+  int i0 = 0;
+#pragma unroll
+  for (int ng = CT; ng >= 1; --ng) {
+    while (i0 <= kmx[ng - 1]) {  // uniform
+#pragma unroll
+      for (int d = 0; d < PF; ++d) {
+        const int i = i0 + kq;
+        double a[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) a[m] = Z[za[m] + i0];
+#pragma unroll
+        for (int g = 0; g < ng; ++g) {
+          const double b = i <= jv[g] ? bq[d][g] : 0.0;
+#pragma unroll
+          for (int m = 0; m < MT; ++m) acc[g][m] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b, acc[g][m], 0, 0, 0);
+        }
+        load_next(bq[d]);
+        i0 += 4;
       }
     }
   }
@@ -656,6 +739,9 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
 #ifndef TCI_DRAWS_ABLATE
 #define TCI_DRAWS_ABLATE 0  // diagnostics only (wrong results): bit0 no normals, bit1 no MFMA, bit2 no scalars
 #endif
+#ifndef TCI_DRAWS_WPE
+#define TCI_DRAWS_WPE 4  // waves per SIMD k_draws is compiled for (<= 128 VGPRs)
+#endif
 constexpr int kDrawsPF = 2;               // R values prefetched this many k-steps ahead (mfma_zr PF)
 constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each)
 constexpr int kDrawSteps = 8 * kDrawMT;   // steps per pass (2 rows per step)
@@ -665,7 +751,8 @@ enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a d
 // FP64 R is read from global memory (L2) with a kDrawsPF-deep prefetch: staging it in LDS beside the
 // normals (74 KB at P = 136) left one workgroup per CU, and that layout took 144 us per TestData
 // chunk against 105 us with R from L2 and four 35 KB workgroups per CU (r03n/r03o).
-__host__ __device__ inline int64_t draws_lds_bytes(int64_t L) { return (2 * kDrawSteps * L) * 8 + 16; }
+// (+ 8 doubles: mfma_zr_pf's reads past the last row's P entries, zeroed with the pads)
+__host__ __device__ inline int64_t draws_lds_bytes(int64_t L) { return (2 * kDrawSteps * L + 8) * 8; }
 // Passes per workgroup: every workgroup reads the chain's R once per pass. FUSED (a few hundred
 // chains): 2 (1: 108.8, 2: 104.7, 4: 123.7 us per TestData chunk); WALK (thousands of chains, P =
 // 207): 4, fewer and longer workgroups reading R fewer times.
@@ -675,7 +762,7 @@ __host__ __device__ inline int draws_passes(bool walk) { return walk ? 4 : 2; }
 // rows loop over calls. The wave count and CT only move column tiles between waves and calls: same
 // bits.
 template <int NWD, int CT>
-__global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end, int npass) {
+__global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(TCI_DRAWS_WPE))) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end, int npass) {
   constexpr int kDrawWaves = NWD, kDrawThreads = 64 * NWD;
   constexpr int kDrawCT = CT;
   extern __shared__ __attribute__((aligned(16))) double dyn[];
@@ -688,6 +775,9 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
   const int64_t DW = draw_stride(ld);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   double* Z = dyn;
+  // finite LDS under every z*R read (mfma_zr_pf): the pads past P and past the last row stay zero
+  for (int e = threadIdx.x; e < 2 * kDrawSteps * L + 8; e += kDrawThreads) Z[e] = 0.0;
+  __syncthreads();
   const double* Rg = st.Rd + c * tri_stride(ld);
   const double a = 0.5 * (double)st.nobs[c];
   const double inv_ds = 1.0 / p.drscale;
@@ -703,7 +793,7 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
     const auto put = [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; };
     if (!(TCI_DRAWS_ABLATE & 2))
       for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT)
-        mfma_zr<kDrawMT, kDrawCT, kDrawWaves, decltype(put), kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
+        mfma_zr_pf<kDrawMT, kDrawCT, kDrawWaves, kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
     for (int k = w; k < ns; k += kDrawWaves) {
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
       if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
@@ -716,7 +806,7 @@ __global__ __launch_bounds__(64 * NWD) void k_draws(DramState st, DramParams p, 
     double* sc = drow + step * DW + 2 * ld;
     sc[D_U1] = uniform_at(p.seed, key, step, P_U1);
     sc[D_U2] = uniform_at(p.seed, key, step, P_U2);
-    sc[D_G] = p.updatesigma ? gamma_unit(p.seed, key, step, a) : 1.0;
+    sc[D_G] = p.updatesigma ? gamma_unit_t(p.seed, key, step, a) : 1.0;
   }
 }
 
@@ -972,14 +1062,12 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   constexpr int NW = kThreads / 64;
   constexpr int D = 2 * EPW;                // steps per round
   constexpr int NS = 2 * D;                 // proposal slots
-  // candidate rows for the next round: row s + a1 + 1 + k for k < NC. EPW = 1: both (k = 0, 1);
+  // candidate rows for the next round: row s + a1 + 1 + k for k < D + 2 (EPW - 1). EPW = 1: both (k = 0, 1);
   // EPW = 2: the rows of an advance by 1 or 4 (k = 0, 2, 3, 5) -- an advance by 2 or 3 loads its
   // missing row (k = 1 or 4) after the decisions: six prefetched rows exceeded the 256-register
   // budget of two chains per CU
-  constexpr int NC = D + 2 * (EPW - 1);
   constexpr int NPF = EPW == 1 ? 2 : 4;
   constexpr int kPf[4] = {0, EPW == 1 ? 1 : 2, 3, 5};  // prefetched k (the first NPF)
-  constexpr int NSC = 4 * (2 * D - 1);      // lanes of scalar draws: rows s + 1 .. s + 2D - 1
   __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each evaluating wave's tables
   __shared__ double yl[2][NS][64 * NJ];                         // by round parity: every proposal
   __shared__ double xch[2][NS][4];                              // by round parity: ss, prior, in-bounds
@@ -1028,7 +1116,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   int64_t prow = 0;  // rows prow .. prow + padv - 1 were decided by the previous round (logs pending);
   int padv = 0;      // all but the last did not move the chain (their state is thp)
   // Loads one round ahead. The next round starts at step s + 1 .. s + D, so a round loads every
-  // candidate at its START (this wave's offsets of rows s + a1 + 1 .. s + a1 + NC, and the scalar
+  // candidate at its START (this wave's offsets of rows s + a1 + 1 .. s + a1 + D + 2 (EPW - 1), and the scalar
   // draws of rows s + 1 .. s + 2D - 1) and the next round picks its rows: a whole round hides the
   // latency. The scalar draws are vector loads (lane j: row r0 + j / 4, slot j % 4) read by
   // readlane: scalar loads would also be waited for at the evaluation's first LDS wait.
@@ -1041,7 +1129,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       u[k] = lane + 64 * k < P ? v : 0.0;
     }
   };
-  auto load_sc = [&](int64_t r0) {  // lanes >= NSC load a valid entry that is never read
+  auto load_sc = [&](int64_t r0) {  // lanes >= 4 (2D - 1) load a valid entry that is never read
     return dchain[(int)(min(r0 + (lane >> 2), s_end) - s_begin) * DWi + 2 * ldi + (lane & 3)];
   };
   double ucur[EPW][NJ], cand[NPF][NJ];
@@ -1567,10 +1655,10 @@ template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    int with_records, hipStream_t stream) {
   const size_t lds = (size_t)draws_lds_bytes(st.ld);
-  // 4-wave workgroups, 2 column tiles x 2 row tiles per wave and MFMA call (164 VGPRs: three
+  // 4-wave workgroups, 2 column tiles x 2 row tiles per wave and MFMA call (128 VGPRs: four
   // workgroups per CU). Config 4 (WALK, P = 207): 72.7 ms per 1,000 steps with the 8-wave, 2-tile
   // form -> 53.6 (3 tiles: 58.0, 5: 56.4); TestData (FUSED): 105.3 -> 99.8 us per chunk against
-  // 3 tiles (r03t4, r03u).
+  // 3 tiles (r03t4, r03u); the pipelined z*R loop (mfma_zr_pf) 97.6 -> 86.5 (r04g).
   auto kd = k_draws<4, 2>;
   if (ensure_dyn_lds((const void*)kd, lds) != TCI_OK) return TCI_EHIP;
   const int npass = draws_passes(p.walk != 0);
