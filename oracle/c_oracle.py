@@ -140,6 +140,25 @@ def philox(ctr, key):
     return (r.x, r.y, r.z, r.w)
 
 
+def box_muller_pair(u1, u2):
+    """The restatement's (and the GPU's) Box-Muller transcendental pair, elementwise:
+    (-2 log u1, sin(2 pi u2), cos(2 pi u2)) in plain correctly-rounded FP64 arithmetic."""
+    L = lib()
+    L.bm_neg2log.argtypes = [C.c_double]
+    L.bm_neg2log.restype = C.c_double
+    L.bm_sincospi.argtypes = [C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.bm_sincospi.restype = None
+    u1 = np.asarray(u1, np.float64).ravel()
+    u2 = np.asarray(u2, np.float64).ravel()
+    lg = np.array([L.bm_neg2log(float(v)) for v in u1])
+    sn, cs = np.empty(len(u2)), np.empty(len(u2))
+    a, b = C.c_double(), C.c_double()
+    for i, v in enumerate(u2):
+        L.bm_sincospi(2.0 * float(v), C.byref(a), C.byref(b))
+        sn[i], cs[i] = a.value, b.value
+    return lg, sn, cs
+
+
 def dram_run(cells, construct, cell_id, theta0, lower, upper, prior_mu, prior_sig, qcov_diag, sigma2_0, opts,
              keys=None, want_chain=False, want_R=False, nthreads=0):
     """mcmcrun's DRAM restated on the CPU (oracle/tci_dram_oracle.c), one chain per row, with the C

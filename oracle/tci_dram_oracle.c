@@ -24,7 +24,8 @@
  *   summaries mean / std(., 1) of rows stats_from..end (:284-301), sqrt(mean(s2chain)) and
  *             std(sqrt(s2chain), 1) over every row (:302-303)
  * The random numbers are the GPU sampler's streams (Philox4x32-10 keyed by (seed), counter (chain
- * key, step, purpose, index); FP64 Box-Muller normals; Marsaglia-Tsang Gamma), so for the same
+ * key, step, purpose, index); FP64 Box-Muller normals in the GPU's own arithmetic (bm_*), bit for
+ * bit; Marsaglia-Tsang Gamma), so for the same
  * inputs this chain and the GPU's agree up to the rounding of the continuous arithmetic (the
  * GPU's SS summation order, its pairwise covariance merge, its Cholesky order): a GPU test checks
  * that (tests/test_dram_gpu.py), and bench.py times this restatement as config 1's CPU fit.
@@ -90,35 +91,71 @@ static double u01(uint32_t a, uint32_t b) {
   return ((double)x + 0.5) * 0x1p-53;
 }
 
-/* sin(pi x), cos(pi x) for x in (0, 2), reduced exactly to |r| <= 1/4 */
-static void sincospi(double x, double *s, double *c) {
-  double q = floor(4.0 * x + 0.5);       /* x = q/4 + r, |r| <= 1/8 (exact in binary) */
-  const double r = x - 0.25 * q;
-  const int k = (int)q & 7;
-  const double sr = sin(M_PI * r), cr = cos(M_PI * r);
-  static const double s2 = 0.70710678118654752440;
-  double sv, cv;
-  switch (k) {  /* angle q pi/4 + pi r */
-    case 0: sv = sr; cv = cr; break;
-    case 1: sv = s2 * (sr + cr); cv = s2 * (cr - sr); break;
-    case 2: sv = cr; cv = -sr; break;
-    case 3: sv = s2 * (cr - sr); cv = -s2 * (sr + cr); break;
-    case 4: sv = -sr; cv = -cr; break;
-    case 5: sv = -s2 * (sr + cr); cv = s2 * (sr - cr); break;
-    case 6: sv = -cr; cv = sr; break;
-    default: sv = s2 * (sr - cr); cv = s2 * (sr + cr); break;
+/* Box-Muller's transcendental pair as the GPU computes it (csrc/tci_dram.hip bm_neg2log,
+ * bm_sincospi): correctly rounded +, *, /, sqrt and fma only, operation for operation, so the
+ * normals are the GPU's bits. -2 log(u): u = m 2^e, m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s),
+ * s = (m - 1)/(m + 1), the odd series to s^19; e ln 2 as fdlibm's ln2_hi + ln2_lo. */
+double bm_neg2log(double u) {
+  int e;
+  double m = frexp(u, &e); /* [1/2, 1) */
+  if (m < 0.70710678118654752440) {
+    m = m * 2.0;
+    e = e - 1;
   }
-  *s = sv;
-  *c = cv;
+  const double sv = (m - 1.0) / (m + 1.0);
+  const double z = sv * sv;
+  double q = 1.0 / 19;
+  q = fma(q, z, 1.0 / 17);
+  q = fma(q, z, 1.0 / 15);
+  q = fma(q, z, 1.0 / 13);
+  q = fma(q, z, 1.0 / 11);
+  q = fma(q, z, 1.0 / 9);
+  q = fma(q, z, 1.0 / 7);
+  q = fma(q, z, 1.0 / 5);
+  q = fma(q, z, 1.0 / 3);
+  const double lm = fma(sv * z, q, sv);
+  const double de = (double)e;
+  return -2.0 * (de * 6.93147180369123816490e-01 + (2.0 * lm + de * 1.90821492927058770002e-10));
+}
+
+/* sin(pi x), cos(pi x), x in (0, 2): t = 2x quarter turns, r = t - rint(t) (exact), the Taylor
+ * series of sin / cos((pi/2) r) to r^17 / r^16, then the quadrant */
+void bm_sincospi(double x, double *sn, double *cs) {
+  const double t = 2.0 * x;
+  const double n = rint(t);
+  const double r = t - n, r2 = r * r;
+  double ps = 6.0669357311061955e-12;
+  ps = fma(ps, r2, -6.688035109811468e-10);
+  ps = fma(ps, r2, 5.692172921967927e-08);
+  ps = fma(ps, r2, -3.598843235212085e-06);
+  ps = fma(ps, r2, 0.00016044118478735983);
+  ps = fma(ps, r2, -0.004681754135318688);
+  ps = fma(ps, r2, 0.07969262624616705);
+  ps = fma(ps, r2, -0.6459640975062463);
+  ps = fma(ps, r2, 1.5707963267948966);
+  const double sp = ps * r;
+  double pc = 6.565963114979473e-11;
+  pc = fma(pc, r2, -6.386603083791852e-09);
+  pc = fma(pc, r2, 4.710874778818172e-07);
+  pc = fma(pc, r2, -2.5202042373060607e-05);
+  pc = fma(pc, r2, 0.0009192602748394266);
+  pc = fma(pc, r2, -0.02086348076335296);
+  pc = fma(pc, r2, 0.25366950790104803);
+  pc = fma(pc, r2, -1.2337005501361697);
+  const double cp = fma(pc, r2, 1.0);
+  const int k = (int)n & 3;
+  const double a = (k & 1) ? cp : sp, b = (k & 1) ? sp : cp;
+  *sn = (k & 2) ? -a : a;
+  *cs = ((k + 1) & 2) ? -b : b;
 }
 
 /* z[0..P) of stream (chain, step, purpose): Box-Muller, 2 normals per Philox call */
 static void normals(uint64_t seed, int64_t key, int64_t step, uint32_t purpose, int P, double *z) {
   for (int q = 0; 2 * q < P; ++q) {
     const u32x4 r = rng(seed, key, step, purpose, (uint32_t)q);
-    const double rad = sqrt(-2.0 * log(u01(r.x, r.y)));
+    const double rad = sqrt(bm_neg2log(u01(r.x, r.y)));
     double sn, cs;
-    sincospi(2.0 * u01(r.z, r.w), &sn, &cs);
+    bm_sincospi(2.0 * u01(r.z, r.w), &sn, &cs);
     z[2 * q] = rad * cs;
     if (2 * q + 1 < P) z[2 * q + 1] = rad * sn;
   }

@@ -111,3 +111,28 @@ def test_sigma2_gibbs_law(c_oracle, cells, construct):
     nobs = np.array(nobs, np.float64)
     assert abs(ratio.mean() - np.mean(nobs / (nobs - 2))) < 0.012, ratio.mean()
     assert abs(ratio.std() - np.sqrt(np.mean(2 / nobs))) < 0.015, ratio.std()
+
+
+def test_box_muller_pair_accuracy(c_oracle):
+    """The normals' transcendental pair (the GPU's bm_neg2log / bm_sincospi, restated bit for bit):
+    -2 log u within 2 ulp of libm's on 53-bit uniforms including both ends, sin / cos(2 pi u)
+    within 3e-16 of a long-double reference (0 <= |.| <= 1), quarter turns exact."""
+    import math
+
+    rng = np.random.default_rng(1)
+    n = 20000
+    u = (np.floor(rng.random(n) * 2.0 ** 53) + 0.5) * 2.0 ** -53
+    u1 = np.concatenate([u, 1 - np.arange(1, 200) * 2.0 ** -53, np.arange(1, 200) * 2.0 ** -53 + 2.0 ** -54])
+    quarter = np.arange(1, 8) / 8.0
+    u2 = np.concatenate([u[::-1], quarter, [2.0 ** -53, 1 - 2.0 ** -53]])
+    lg, _, _ = c_oracle.box_muller_pair(u1, u1[:1])
+    ref = np.array([-2.0 * math.log(v) for v in u1])
+    assert np.max(np.abs(lg - ref) / np.spacing(np.abs(ref))) <= 2.0
+    _, sn, cs = c_oracle.box_muller_pair(u2[:1], u2)
+    pil = np.longdouble("3.14159265358979323846264338327950288")
+    th = 2 * pil * u2.astype(np.longdouble)
+    assert np.max(np.abs((sn - np.sin(th)).astype(np.float64))) < 3e-16
+    assert np.max(np.abs((cs - np.cos(th)).astype(np.float64))) < 3e-16
+    k = len(u)
+    np.testing.assert_array_equal(sn[k + 1:k + 7:2], [1.0, 0.0, -1.0])  # quarter turns: r = 0
+    np.testing.assert_array_equal(cs[k + 1:k + 7:2], [0.0, -1.0, 0.0])

@@ -687,7 +687,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(prior, double, n);
   TCI_ALLOC(sigma2, double, n);
   TCI_ALLOC(Rd, double, n * tci::dram_tri_stride(L));
-  TCI_ALLOC(cov, double, n * L2);
+  TCI_ALLOC(cov, double, n * tci::dram_cov_stride(L));
   TCI_ALLOC(work, double, p_max_all > 208 ? n * (size_t)((L + 15) / 16 * 16) * ((L + 15) / 16 * 16) : 1);
   TCI_ALLOC(cmean, double, n * L);
   TCI_ALLOC(wsum, double, n);

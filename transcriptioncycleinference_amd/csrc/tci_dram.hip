@@ -65,7 +65,8 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
     const uint64_t p0 = mul64(0xD2511F53u, c.x), p1 = mul64(0xCD9E8D57u, c.z);
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    c = make_uint4(__builtin_amdgcn_bitop3_b32(hi1, c.y, k.x, 0x96), lo1, __builtin_amdgcn_bitop3_b32(hi0, c.w, k.y, 0x96),
+                   lo0);  // 0x96: three-input xor
     k.x += 0x9E3779B9u;
     k.y += 0xBB67AE85u;
   }
@@ -90,13 +91,73 @@ __device__ __forceinline__ double u01(uint32_t a, uint32_t b) {
 // 5-7 % faster fits, profiles/r02_likelihood/r02k_dram_libs.jsonl; not worth the narrower proposals.)
 constexpr int kNPer = 2;
 
+// The transcendental pair in plain FP64 arithmetic -- correctly rounded +, *, /, sqrt and fma
+// only, so the CPU restatement (oracle/tci_dram_oracle.c: bm_neg2log, bm_sincospi) repeats them
+// bit for bit -- at about half the instructions of the libm log and sincospi (each within ~2 ulp).
+//   -2 log(u), u in (0, 1): u = m 2^e, m in [sqrt(1/2), sqrt(2)); log m = 2 atanh(s) with
+//   s = (m - 1)/(m + 1), |s| < 0.1716: s (1 + z/3 + .. + z^9/19), z = s^2 (truncation < 1e-19);
+//   e ln 2 as fdlibm's ln2_hi (32 bits: e ln2_hi is exact) + ln2_lo.
+__device__ __forceinline__ double bm_neg2log(double u) {
+  double m = __builtin_amdgcn_frexp_mant(u);  // [1/2, 1)
+  int e = __builtin_amdgcn_frexp_exp(u);
+  if (m < 0.70710678118654752440) {
+    m = m * 2.0;
+    e = e - 1;
+  }
+  const double sv = (m - 1.0) / (m + 1.0);
+  const double z = sv * sv;
+  double q = 1.0 / 19;
+  q = fma(q, z, 1.0 / 17);
+  q = fma(q, z, 1.0 / 15);
+  q = fma(q, z, 1.0 / 13);
+  q = fma(q, z, 1.0 / 11);
+  q = fma(q, z, 1.0 / 9);
+  q = fma(q, z, 1.0 / 7);
+  q = fma(q, z, 1.0 / 5);
+  q = fma(q, z, 1.0 / 3);
+  const double lm = fma(sv * z, q, sv);  // log(m) / 2
+  const double de = (double)e;
+  return -2.0 * (de * 6.93147180369123816490e-01 + (2.0 * lm + de * 1.90821492927058770002e-10));
+}
+//   sin(pi x), cos(pi x) for x in (0, 2): t = 2x quarter turns, n = rint(t), r = t - n in
+//   [-1/2, 1/2] (exact); phi = (pi/2) r by its Taylor series to r^17 / r^16 (truncation < 1e-17),
+//   then the quadrant n mod 4.
+__device__ __forceinline__ void bm_sincospi(double x, double& sn, double& cs) {
+  const double t = 2.0 * x;
+  const double n = __builtin_rint(t);
+  const double r = t - n, r2 = r * r;
+  double ps = 6.0669357311061955e-12;
+  ps = fma(ps, r2, -6.688035109811468e-10);
+  ps = fma(ps, r2, 5.692172921967927e-08);
+  ps = fma(ps, r2, -3.598843235212085e-06);
+  ps = fma(ps, r2, 0.00016044118478735983);
+  ps = fma(ps, r2, -0.004681754135318688);
+  ps = fma(ps, r2, 0.07969262624616705);
+  ps = fma(ps, r2, -0.6459640975062463);
+  ps = fma(ps, r2, 1.5707963267948966);
+  const double sp = ps * r;
+  double pc = 6.565963114979473e-11;
+  pc = fma(pc, r2, -6.386603083791852e-09);
+  pc = fma(pc, r2, 4.710874778818172e-07);
+  pc = fma(pc, r2, -2.5202042373060607e-05);
+  pc = fma(pc, r2, 0.0009192602748394266);
+  pc = fma(pc, r2, -0.02086348076335296);
+  pc = fma(pc, r2, 0.25366950790104803);
+  pc = fma(pc, r2, -1.2337005501361697);
+  const double cp = fma(pc, r2, 1.0);
+  const int k = (int)n & 3;
+  const double a = (k & 1) ? cp : sp, b = (k & 1) ? sp : cp;  // sin, cos of (pi/2)(k & 1) + phi, up to sign
+  sn = (k & 2) ? -a : a;
+  cs = ((k + 1) & 2) ? -b : b;
+}
+
 __device__ __forceinline__ void normals_at(uint64_t seed, int64_t c, int64_t step, uint32_t purpose, int item,
                                            double (&z)[kNPer]) {
   const uint4 r = rng(seed, c, step, purpose, (uint32_t)item);
   const double u1 = u01(r.x, r.y), u2 = u01(r.z, r.w);
-  const double rad = sqrt(-2.0 * log(u1));
+  const double rad = sqrt(bm_neg2log(u1));
   double sn, cs;
-  sincospi(2.0 * u2, &sn, &cs);  // one reduction for both, exact in units of pi
+  bm_sincospi(2.0 * u2, sn, cs);
   z[0] = rad * cs;
   z[1] = rad * sn;
 }
@@ -515,8 +576,8 @@ __global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* _
   if (c >= st.n_chains) return;
   const int64_t ld = st.ld;
   const int P = st.npar[c];
-  double* cv = st.cov + c * ld * ld;
-  for (int64_t e = threadIdx.x; e < ld * ld; e += kThreads) cv[e] = 0.0;
+  double* cv = st.cov + c * dram_cov_stride(ld);
+  for (int64_t e = threadIdx.x; e < dram_cov_stride(ld); e += kThreads) cv[e] = 0.0;
   for (int64_t e = threadIdx.x; e < tri_stride(ld); e += kThreads) st.Rd[c * tri_stride(ld) + e] = 0.0;
   __syncthreads();
   for (int j = threadIdx.x; j < P; j += kThreads) {
@@ -549,7 +610,8 @@ __global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* _
 // Every sum runs over the window's rows in row order from 0.0, so every engine has the same bits:
 // k_chain adds each row as it is decided (ColAcc / S2Acc on its record waves; a window that spans
 // chunks continues from DramState::wsumv / wacc1 / wacc2 / s2acc), k_walk and k_stats read the
-// window's logs back at its end (window_records).
+// window's logs back at its end (window_records, window_s2_records). (Summing the s2 log at the
+// window's end in k_chain too: 226.9 -> 228.4 us per chunk, r04j.)
 __device__ __forceinline__ int64_t log_slot(const DramParams& p, int64_t row) { return (row - 1) % p.win; }
 
 // The batched engine's per-step log (one workgroup per chain).
@@ -923,8 +985,8 @@ struct ColAcc {
 // The same for s2 (one value per row; lane 0 of k_chain's kSigWave, uniform in window_records).
 struct S2Acc {
   double sum, S1, S2, K;
-  __device__ __forceinline__ void add(double s2) {
-    const double dq = sqrt(s2) - K;
+  __device__ __forceinline__ void add(double s2) { add_dq(s2, sqrt(s2) - K); }
+  __device__ __forceinline__ void add_dq(double s2, double dq) {  // dq = sqrt(s2) - K
     sum = sum + s2;
     S1 = S1 + dq;
     S2 = fma(dq, dq, S2);
@@ -938,9 +1000,9 @@ struct S2Acc {
   }
 };
 
-// The s2 records of the window ending at row `last` from its log, by one wave: 64 rows per pass in
-// lanes, added in row order through lane broadcasts (S2Acc::add, as k_chain adds them);
-// with_out: also the thinned s2 rows.
+// The s2 records of the window ending at row `last` from its log, by one wave (k_chain, k_walk): 64
+// rows per pass in lanes, sqrt(s2) - K lane-parallel, then added in row order through lane
+// broadcasts (S2Acc::add's arithmetic); with_out: also the thinned s2 rows.
 __device__ void window_s2_records(const DramState& st, const DramParams& p, int64_t c, int64_t last, int lane,
                                   bool with_out) {
   const int64_t first = win_first(p, last);
@@ -952,8 +1014,9 @@ __device__ void window_s2_records(const DramState& st, const DramParams& p, int6
     const double v = lg[min(r, nrow - 1)];
     int64_t k;
     if (with_out && st.s2_out != nullptr && r < nrow && kept_row(p, first + r, k)) st.s2_out[k * st.n_chains + c] = v;
+    const double dq = sqrt(v) - q.K;
     const int m = min(64, nrow - r0);
-    for (int l = 0; l < m; ++l) q.add(lane_bcast(v, l));
+    for (int l = 0; l < m; ++l) q.add_dq(lane_bcast(v, l), lane_bcast(dq, l));
   }
   if (lane == 0) q.finish(st, c, first, last);
 }
@@ -1806,7 +1869,10 @@ __device__ __forceinline__ void chol16_finish(double (&a)[4], int lane, double* 
 // Instances: NW waves per workgroup (one chain), MAXT = max tiles per dimension, kAdOwn output tiles
 // per wave (MAXT (MAXT + 1) / 2 <= NW kAdOwn): <8, 9, 6> for P <= 144 (two chains per CU at 128
 // VGPRs), <8, 13, 12> for P <= 208 (configs 4/5: 200 points, P = 207; one chain per CU).
-constexpr int kAdRB = 16;   // window rows per LDS batch
+#ifndef TCI_AD_RB
+#define TCI_AD_RB 16
+#endif
+constexpr int kAdRB = TCI_AD_RB;  // window rows per LDS batch
 __host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P) {
   const int64_t NT = (P + 15) / 16, LX = 16 * NT;
   const int64_t shared = kAdRB * LX > 2 * NT * 256 ? kAdRB * LX : 2 * NT * 256;  // X | panel buffers
@@ -1820,8 +1886,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   constexpr int kAdM = MAXT;
   constexpr int NTH = 64 * NW;
   static_assert(MAXT * (MAXT + 1) / 2 <= NW * kAdOwn, "owned tiles per wave");
-  // merge groups: every old value of a group's tiles is read before any of them is written (a
-  // diagonal tile reads the mirrors of its own elements; tiles never share an element)
+  // merge groups: the old covariance values of kAdMG tiles in flight at once (the register budget)
   constexpr int kAdMG = kAdOwn <= 6 ? 3 : 6;
   static_assert(kAdOwn % kAdMG == 0, "owned tiles come in whole merge groups");
   extern __shared__ __attribute__((aligned(16))) double dyn[];
@@ -1841,7 +1906,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   double* Pb = dyn;               // Cholesky: panel buffers [2][NT][256] (aliases X)
   double* mb = dyn + shared;      // batch mean
   double* mo = mb + LX;           // old mean
-  double* cvg = st.cov + c * ld * ld;
+  double* cvg = st.cov + c * dram_cov_stride(ld);
   double* mu = st.cmean + c * ld;
   const int nb = (TCI_ADAPT_ABLATE & 2) ? 0 : (int)p.adaptint;
   const double* win = st.window + c * p.win * ld;
@@ -1912,8 +1977,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   //      become the matrix to factor: cov + qcovadj I (identity in the padding)
   const double na = st.wsum[c], nn = na + (double)p.adaptint;
   const double fcross = na * (double)p.adaptint / nn;
-  // in groups of kAdMG tiles: a group's old values are all read before any of them is written (a
-  // diagonal tile reads the mirrors of its own elements)
+  // cov in the owned-tile layout: tile k (row-major upper-tile order; wave w's slot o is tile
+  // w + NW o) at cvg + 256 k, accumulator entry q of lane l at 64 q + l -- four 512-byte reads per
+  // tile, and a diagonal tile keeps both triangles (the scatter, the update and hence the stored
+  // values are symmetric bit for bit: the products and sums of (i, j) and (j, i) are the same)
   const double rn1 = 1.0 / (nn - 1.0);
 #pragma unroll
   for (int o0 = 0; o0 < kAdOwn; o0 += kAdMG) {
@@ -1923,9 +1990,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
     for (int u = 0; u < kAdMG; ++u)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int o = o0 + u, i = 16 * sti[o] + kq + 4 * q, j = 16 * stj[o] + row;
-        old[u][q] = (o < nown && i < P && j < P && na > 0.0) ? cvg[i <= j ? (int64_t)i * ld + j : (int64_t)j * ld + i]
-                                                            : 0.0;
+        const int o = o0 + u;
+        old[u][q] = (o < nown && na > 0.0) ? cvg[256 * (w + NW * o) + 64 * q + lane] : 0.0;
       }
 #pragma unroll
     for (int u = 0; u < kAdMG; ++u) {
@@ -1934,9 +2000,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int i = 16 * sti[o] + kq + 4 * q, j = 16 * stj[o] + row;
-        double a;
+        double a, cv = 0.0;
         if (i < P && j < P) {
-          double cv;
           if (nn <= 1.0) {
             cv = 0.0;  // a single row so far: covariance 0 (the recurrence's first row)
           } else if (na == 0.0) {
@@ -1945,11 +2010,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
             const double di = mb[i] - mo[i], dj = mb[j] - mo[j];
             cv = (old[u][q] * (na - 1.0) + acc[o][q] + di * dj * fcross) * rn1;
           }
-          if (i <= j) cvg[(int64_t)i * ld + j] = cv;
           a = cv + (i == j ? p.qcovadj : 0.0);
         } else {
           a = i == j ? 1.0 : 0.0;
         }
+        cvg[256 * (w + NW * o) + 64 * q + lane] = cv;
         acc[o][q] = a;
       }
     }
@@ -1974,41 +2039,54 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   }
   __syncthreads();
   TCI_APHASE(2)
-  // ---- blocked Cholesky U'U of the owned tiles; panel row pk goes through LDS buffer pk & 1
-  bool ok = true;
-  for (int pk = 0; pk < ((TCI_ADAPT_ABLATE & 1) ? 0 : NT); ++pk) {
-    double* B = Pb + (pk & 1) * NT * 256;  // tile (pk, tj) at B + 256 tj
-    double* D = B + 256 * pk;
-    // (1) row pk to LDS; the diagonal tile is factored in its owner's registers on the way
-    double dt[4] = {0.0, 0.0, 0.0, 0.0};
-    bool own_diag = false;
+  // ---- blocked Cholesky U'U of the owned tiles; panel row pk goes through LDS buffer pk & 1.
+  // Look-ahead: the trailing update of panel pk ends with row pk + 1 -- the owners store its tiles
+  // to the next buffer and the owner of the diagonal tile factors it right away, while the other
+  // waves still apply their updates (the one-wave factorization no longer waits for them).
+  const bool chol = !(TCI_ADAPT_ABLATE & 1);
+  // row pr's tiles to LDS buffer pr & 1; the diagonal one (slot od) factored by its owner
+  auto panel_row = [&](int pr) {
+    double* Bn = Pb + (pr & 1) * NT * 256;
+    int od = -1;
 #pragma unroll
     for (int o = 0; o < kAdOwn; ++o) {
-      if (o >= nown || sti[o] != pk) continue;  // uniform
-      if (stj[o] == pk) {
-        own_diag = true;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dt[q] = acc[o][q];
+      if (o >= nown || sti[o] != pr) continue;  // uniform
+      if (stj[o] == pr) {
+        od = o;
       } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) B[256 * stj[o] + (kq + 4 * q) * 16 + row] = acc[o][q];
+        for (int q = 0; q < 4; ++q) Bn[256 * stj[o] + (kq + 4 * q) * 16 + row] = acc[o][q];
       }
     }
-    if (own_diag) {  // uniform
+    if (od >= 0) {  // uniform
+      double dt[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double v = acc[0][q];
+#pragma unroll
+        for (int o = 1; o < kAdOwn; ++o) v = od == o ? acc[o][q] : v;
+        dt[q] = v;
+      }
       bool bad = false;
       chol16_step2<0>(dt, lane, rdg, bad);
       wave_sync();
       chol16_finish(dt, lane, rdg, rdg);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) D[(kq + 4 * q) * 16 + row] = dt[q];
+      for (int q = 0; q < 4; ++q) Bn[256 * pr + (kq + 4 * q) * 16 + row] = dt[q];
       if (bad && lane == 0) fail = 1;
     }
-    __syncthreads();
-    TCI_APHASE(3)
-    if (fail) {
+  };
+  bool ok = true;
+  if (chol) panel_row(0);
+  __syncthreads();
+  TCI_APHASE(3)
+  for (int pk = 0; pk < (chol ? NT : 0); ++pk) {
+    if (fail) {  // uniform (read after a barrier)
       ok = false;
       break;
     }
+    double* B = Pb + (pk & 1) * NT * 256;  // tile (pk, tj) at B + 256 tj
+    const double* D = B + 256 * pk;
     // (2) the panel's row tiles (pk, tj > pk): U_pk' X = A -> X, one column per lane
     {
       const int g = w * 4 + kq;  // 16-lane group 0 .. 4 NW - 1
@@ -2029,7 +2107,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
     }
     __syncthreads();
     TCI_APHASE(5)
-    // (3) the owners take row pk of U back; trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj
+    // (3) the owners take row pk of U back; trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj;
+    //     then row pk + 1 to the other buffer, its diagonal tile factored (look-ahead)
 #pragma unroll
     for (int o = 0; o < kAdOwn; ++o) {
       if (o >= nown) continue;  // uniform
@@ -2045,6 +2124,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
                                                         0, 0);
       }
     }
+    if (pk + 1 < NT) panel_row(pk + 1);
+    __syncthreads();
     TCI_APHASE(0)
   }
   if (ok && !(TCI_ADAPT_ABLATE & 1)) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
@@ -2127,7 +2208,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
   double* X = dyn;           // a batch of centred window rows [rb][LX]
   double* mb = X + rb * LX;  // batch mean
   double* mo = mb + LX;      // old mean
-  double* cvg = st.cov + c * ld * ld;
+  double* cvg = st.cov + c * dram_cov_stride(ld);
   double* mu = st.cmean + c * ld;
   const int64_t LT = gt_lt(ld);
   double* Wt = st.work + c * LT * LT;

@@ -13,6 +13,11 @@ namespace tci {
 // Doubles per chain of DramState::Rd: the packed triangle ld(ld+1)/2 rounded up to 128 doubles, so a
 // chain's triangle starts 1 KiB-aligned and is copied to LDS in whole 1 KiB pieces (k_draws).
 constexpr int64_t dram_tri_stride(int64_t ld) { return (ld * (ld + 1) / 2 + 127) / 128 * 128; }
+// Doubles per chain of DramState::cov: the ld x ld matrix (k_adapt_gt), or k_adapt_mfma's owned-tile
+// layout (the NT (NT + 1) / 2 upper 16 x 16 tiles of 256 doubles, NT = ceil(ld / 16)), whichever is larger.
+constexpr int64_t dram_cov_stride(int64_t ld) {
+  return ld * ld > (ld + 15) / 16 * ((ld + 15) / 16 + 1) / 2 * 256 ? ld * ld : (ld + 15) / 16 * ((ld + 15) / 16 + 1) / 2 * 256;
+}
 
 struct DramState {
   int64_t n_chains;
@@ -32,7 +37,7 @@ struct DramState {
   double* Rd;              // proposal Cholesky factor R (upper: proposal = theta + z * R) in FP64, as packed
                            // upper triangles (chain c at c * dram_tri_stride(ld)); the
                            // [ld][ld] double form is built on the host for the results only
-  double* cov;             // running chain covariance / mean / weight (mcmcstat covupd)
+  double* cov;             // running chain covariance (mcmcstat covupd), dram_cov_stride(ld) per chain
   double* cmean;
   double* wsum;
   double* window;          // chain rows by window slot (DramParams::win per chain): the covupd window, and
