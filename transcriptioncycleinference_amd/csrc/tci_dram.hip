@@ -1754,6 +1754,22 @@ int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, 
 #define TCI_ADAPT_ABLATE 0  // diagnostics only (wrong results): bit0 skip the Cholesky, bit1 skip the covupd passes
 #endif
 
+// This lane's index computed afresh (v_mbcnt). The adaptation kernels run at their register budget,
+// where the compiler keeps lane-derived indices alive across whole phases and spills them: a scratch
+// reload inside the diagonal factorization or the panel solve puts a memory round trip on a
+// latency-bound path (one per pivot pair, r04 asm). Volatile, so it is recomputed where it is used.
+__device__ __forceinline__ int lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+template <bool F>  // F: lane_now() (a kernel that spills), else threadIdx.x (kept in a register)
+__device__ __forceinline__ int lane_idx() {
+  if constexpr (F) return lane_now();
+  return (int)(threadIdx.x & 63);
+}
+
 // Lane (16 g + K)'s x in every lane of 16-lane row g (DPP row_newbcast, no LDS).
 template <int K>
 __device__ __forceinline__ double row_bcast16(double x) {
@@ -1790,11 +1806,11 @@ __device__ __forceinline__ double row_to_all(double x) {
 // are the one-pivot form's (bitwise-equal fits, r03ag). Half the pivot round trips (readlane ->
 // v_rcp_f64 + Newton -> update -> readlane) of the one wave that factors the tile, ~25 % fewer
 // instructions: k_adapt_mfma 112.2 -> 109.3 us per TestData adaptation (r03af).
-template <int K>
-__device__ __forceinline__ void chol16_step2(double (&a)[4], int lane, double* dpiv, bool& bad) {
+template <int K, bool F = false>
+__device__ __forceinline__ void chol16_step2(double (&a)[4], double* dpiv, bool& bad) {
   if constexpr (K < 16) {
     constexpr int kg0 = K & 3, kr0 = K >> 2, kg1 = (K + 1) & 3, kr1 = (K + 1) >> 2;
-    const int g = lane >> 4, j = lane & 15;
+    const int lane = lane_idx<F>(), g = lane >> 4, j = lane & 15;
     const double d0 = lane_bcast(a[kr0], 16 * kg0 + K);      // A[K][K]
     const double b = lane_bcast(a[kr0], 16 * kg0 + K + 1);   // A[K][K+1]
     const double bl = lane_bcast(a[kr1], 16 * kg1 + K);      // A[K+1][K] (the updates leave the two
@@ -1831,14 +1847,15 @@ __device__ __forceinline__ void chol16_step2(double (&a)[4], int lane, double* d
       dpiv[K] = d0;
       dpiv[K + 1] = d1p;
     }
-    chol16_step2<K + 2>(a, lane, dpiv, bad);
+    chol16_step2<K + 2, F>(a, dpiv, bad);
   }
 }
 
 // After the 16 steps: U[i][j] = A[i][j] / sqrt(d_i) for j >= i; rdg[i] = 1 / U[i][i] for the panel
 // solve (dpiv and rdg may alias: each lane reads its pivots before the diagonal lanes write).
-__device__ __forceinline__ void chol16_finish(double (&a)[4], int lane, double* dpiv, double* rdg) {
-  const int g = lane >> 4, j = lane & 15;
+template <bool F = false>
+__device__ __forceinline__ void chol16_finish(double (&a)[4], double* dpiv, double* rdg) {
+  const int lane = lane_idx<F>(), g = lane >> 4, j = lane & 15;
   double rs[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) rs[q] = 1.0 / sqrt(dpiv[g + 4 * q]);
@@ -1884,6 +1901,7 @@ template <int NW, int MAXT, int kAdOwn, int WPE = (NW <= 8 ? 2 : NW / 4)>  // kA
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_adapt_mfma(
     DramState st, DramParams p) {
   constexpr int kAdM = MAXT;
+  constexpr bool kFresh = WPE >= 4;  // the 128-VGPR instance spills lane-derived indices otherwise
   constexpr int NTH = 64 * NW;
   static_assert(MAXT * (MAXT + 1) / 2 <= NW * kAdOwn, "owned tiles per wave");
   // merge groups: the old covariance values of kAdMG tiles in flight at once (the register budget)
@@ -1892,9 +1910,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   __shared__ int fail;
   __shared__ double rdg[16];  // 1 / U[k][k] of the current diagonal tile
-  const int t = threadIdx.x, lane = t & 63;
+  const int t = threadIdx.x, lane = t & 63;  // lane-derived tile indices: lane_idx<kFresh>() where used
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int row = lane & 15, kq = lane >> 4;
   const int64_t c = blockIdx.x;
   const int64_t step = *st.step;
   if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
@@ -1959,8 +1976,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
     }
     __syncthreads();
     if (r0 + kAdRB < nb) load_batch(r0 + kAdRB);
+    const int lnx = lane_idx<kFresh>();
     for (int k0 = 0; k0 < n; k0 += 4) {
-      const double* xr = X + (k0 + kq) * LX + row;
+      const double* xr = X + (k0 + (lnx >> 4)) * LX + (lnx & 15);
       double xa[kAdOwn], xb[kAdOwn];
 #pragma unroll
       for (int o = 0; o < kAdOwn; ++o) {
@@ -1985,13 +2003,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
   for (int o0 = 0; o0 < kAdOwn; o0 += kAdMG) {
     if (o0 >= nown) break;  // uniform
+    const int ln = lane_idx<kFresh>(), row = ln & 15, kq = ln >> 4;
     double old[kAdMG][4];
 #pragma unroll
     for (int u = 0; u < kAdMG; ++u)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int o = o0 + u;
-        old[u][q] = (o < nown && na > 0.0) ? cvg[256 * (w + NW * o) + 64 * q + lane] : 0.0;
+        old[u][q] = (o < nown && na > 0.0) ? cvg[256 * (w + NW * o) + 64 * q + ln] : 0.0;
       }
 #pragma unroll
     for (int u = 0; u < kAdMG; ++u) {
@@ -2014,7 +2033,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
         } else {
           a = i == j ? 1.0 : 0.0;
         }
-        cvg[256 * (w + NW * o) + 64 * q + lane] = cv;
+        cvg[256 * (w + NW * o) + 64 * q + ln] = cv;
         acc[o][q] = a;
       }
     }
@@ -2047,6 +2066,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   // row pr's tiles to LDS buffer pr & 1; the diagonal one (slot od) factored by its owner
   auto panel_row = [&](int pr) {
     double* Bn = Pb + (pr & 1) * NT * 256;
+    const int ln = lane_idx<kFresh>(), row = ln & 15, kq = ln >> 4;
     int od = -1;
 #pragma unroll
     for (int o = 0; o < kAdOwn; ++o) {
@@ -2068,9 +2088,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
         dt[q] = v;
       }
       bool bad = false;
-      chol16_step2<0>(dt, lane, rdg, bad);
+      chol16_step2<0, kFresh>(dt, rdg, bad);
       wave_sync();
-      chol16_finish(dt, lane, rdg, rdg);
+      chol16_finish<kFresh>(dt, rdg, rdg);
 #pragma unroll
       for (int q = 0; q < 4; ++q) Bn[256 * pr + (kq + 4 * q) * 16 + row] = dt[q];
       if (bad && lane == 0) fail = 1;
@@ -2089,7 +2109,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const double* D = B + 256 * pk;
     // (2) the panel's row tiles (pk, tj > pk): U_pk' X = A -> X, one column per lane
     {
-      const int g = w * 4 + kq;  // 16-lane group 0 .. 4 NW - 1
+      const int ln = lane_idx<kFresh>(), row = ln & 15;
+      const int g = w * 4 + (ln >> 4);  // 16-lane group 0 .. 4 NW - 1
       for (int tj = pk + 1 + g; tj < NT; tj += 4 * NW) {
         double* A = B + 256 * tj;
         double x[16];
@@ -2109,6 +2130,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
     TCI_APHASE(5)
     // (3) the owners take row pk of U back; trailing tiles (ti, tj), pk < ti <= tj: A -= X_ti' X_tj;
     //     then row pk + 1 to the other buffer, its diagonal tile factored (look-ahead)
+    const int ln3 = lane_idx<kFresh>(), row = ln3 & 15, kq = ln3 >> 4;
 #pragma unroll
     for (int o = 0; o < kAdOwn; ++o) {
       if (o >= nown) continue;  // uniform
@@ -2130,6 +2152,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   }
   if (ok && !(TCI_ADAPT_ABLATE & 1)) {  // singular: keep the previous R (mcmcstat: "cmat singular, not adapting")
     const double sc = p.adascale > 0.0 ? p.adascale : 2.4 / sqrt((double)P);
+    const int ln = lane_idx<kFresh>(), row = ln & 15, kq = ln >> 4;
 #pragma unroll
     for (int o = 0; o < kAdOwn; ++o) {
       if (o >= nown) continue;  // uniform
@@ -2334,9 +2357,9 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
       for (int q = 0; q < 4; ++q) dt[q] = A[(kq + 4 * q) * 16 + row];
       bool bad = false;
-      chol16_step2<0>(dt, lane, rdg, bad);
+      chol16_step2<0>(dt, rdg, bad);
       wave_sync();
-      chol16_finish(dt, lane, rdg, rdg);
+      chol16_finish(dt, rdg, rdg);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         A[(kq + 4 * q) * 16 + row] = dt[q];
