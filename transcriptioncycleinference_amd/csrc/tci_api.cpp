@@ -646,7 +646,8 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   // every engine's per-row log.
   const int64_t ai = opt->adaptint;
   const int64_t DW = tci::draw_stride(ld);
-  const int64_t chunk_cap = std::max<int64_t>(32, (int64_t)(((size_t)2 << 30) / (n * (size_t)DW * sizeof(double))));
+  const int64_t chunk_cap =
+      std::max<int64_t>(32, (int64_t)(((size_t)TCI_DRAWS_GIB << 30) / (n * (size_t)DW * sizeof(double))));
   // Without adaptation the window is 100 rows: the records' merge partition (the same for every engine)
   // and the batched engine's graph block stay small (a 1,000-row window made the batched engine run up
   // to 1,000 steps as plain launches before its first graph replay).
@@ -688,7 +689,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(sigma2, double, n);
   TCI_ALLOC(Rd, double, n * tci::dram_tri_stride(L));
   TCI_ALLOC(cov, double, n * tci::dram_cov_stride(L));
-  TCI_ALLOC(work, double, p_max_all > 208 ? n * (size_t)((L + 15) / 16 * 16) * ((L + 15) / 16 * 16) : 1);
+  TCI_ALLOC(work, double, p_max_all > std::min(208, TCI_ADAPT_GT_FROM) ? n * (size_t)((L + 15) / 16 * 16) * ((L + 15) / 16 * 16) : 1);
   TCI_ALLOC(cmean, double, n * L);
   TCI_ALLOC(wsum, double, n);
   TCI_ALLOC(window, double, n * (size_t)win * L);

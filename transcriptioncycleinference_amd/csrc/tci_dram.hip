@@ -801,11 +801,14 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
 #ifndef TCI_DRAWS_ABLATE
 #define TCI_DRAWS_ABLATE 0  // diagnostics only (wrong results): bit0 no normals, bit1 no MFMA, bit2 no scalars
 #endif
+#ifndef TCI_DRAWS_WIDE
+#define TCI_DRAWS_WIDE 1  // WALK: 64-row draws passes (k_draws<8, 2, 4, 2>)
+#endif
 #ifndef TCI_DRAWS_WPE
 #define TCI_DRAWS_WPE 4  // waves per SIMD k_draws is compiled for (<= 128 VGPRs)
 #endif
 constexpr int kDrawsPF = 2;               // R values prefetched this many k-steps ahead (mfma_zr PF)
-constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each)
+constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each), 4-wave workgroups
 constexpr int kDrawSteps = 8 * kDrawMT;   // steps per pass (2 rows per step)
 enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
 
@@ -814,7 +817,13 @@ enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a d
 // normals (74 KB at P = 136) left one workgroup per CU, and that layout took 144 us per TestData
 // chunk against 105 us with R from L2 and four 35 KB workgroups per CU (r03n/r03o).
 // (+ 8 doubles: mfma_zr_pf's reads past the last row's P entries, zeroed with the pads)
-__host__ __device__ inline int64_t draws_lds_bytes(int64_t L) { return (2 * kDrawSteps * L + 8) * 8; }
+__host__ __device__ inline int64_t draws_lds_bytes(int64_t L, int mt = kDrawMT) { return (2 * 8 * mt * L + 8) * 8; }
+// WALK (thousands of chains): their R triangles (171 KB per chain at P = 207, 1.7 GB for config
+// 4) stream from HBM, once per pass, so the passes there are twice as long -- 4 row tiles (64 rows)
+// in an 8-wave workgroup of 256-VGPR waves, one per CU (106 KB of normals): the R traffic per row
+// halves (config 4 ablations, r04t: z*R 1.51 ms of the pass's 2.31 ms per launch).
+constexpr int kDrawMTWalk = 4;
+__host__ __device__ inline bool draws_walk_wide(int64_t L) { return draws_lds_bytes(L, kDrawMTWalk) <= 150 * 1024; }
 // Passes per workgroup: every workgroup reads the chain's R once per pass. FUSED (a few hundred
 // chains): 2 (1: 108.8, 2: 104.7, 4: 123.7 us per TestData chunk); WALK (thousands of chains, P =
 // 207): 4, fewer and longer workgroups reading R fewer times.
@@ -823,10 +832,11 @@ __host__ __device__ inline int draws_passes(bool walk) { return walk ? 4 : 2; }
 // NWD waves per workgroup, CT column tiles per wave and MFMA call (launch_chain_t: 4 and 2); longer
 // rows loop over calls. The wave count and CT only move column tiles between waves and calls: same
 // bits.
-template <int NWD, int CT>
-__global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(TCI_DRAWS_WPE))) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end, int npass) {
+template <int NWD, int CT, int MT = kDrawMT, int WPE = TCI_DRAWS_WPE>
+__global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE))) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end, int npass) {
   constexpr int kDrawWaves = NWD, kDrawThreads = 64 * NWD;
   constexpr int kDrawCT = CT;
+  constexpr int kDrawSteps = 8 * MT;  // steps per pass
   extern __shared__ __attribute__((aligned(16))) double dyn[];
   const int64_t c = blockIdx.x;
   if (c >= st.n_chains) return;
@@ -855,7 +865,7 @@ __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(TCI_DR
     const auto put = [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; };
     if (!(TCI_DRAWS_ABLATE & 2))
       for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT)
-        mfma_zr_pf<kDrawMT, kDrawCT, kDrawWaves, kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
+        mfma_zr_pf<MT, kDrawCT, kDrawWaves, kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
     for (int k = w; k < ns; k += kDrawWaves) {
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
       if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
@@ -1717,17 +1727,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    int with_records, hipStream_t stream) {
-  const size_t lds = (size_t)draws_lds_bytes(st.ld);
+  const bool wide = p.walk != 0 && TCI_DRAWS_WIDE && draws_walk_wide(st.ld);
+  const size_t lds = (size_t)draws_lds_bytes(st.ld, wide ? kDrawMTWalk : kDrawMT);
   // 4-wave workgroups, 2 column tiles x 2 row tiles per wave and MFMA call (128 VGPRs: four
   // workgroups per CU). Config 4 (WALK, P = 207): 72.7 ms per 1,000 steps with the 8-wave, 2-tile
   // form -> 53.6 (3 tiles: 58.0, 5: 56.4); TestData (FUSED): 105.3 -> 99.8 us per chunk against
   // 3 tiles (r03t4, r03u); the pipelined z*R loop (mfma_zr_pf) 97.6 -> 86.5 (r04g).
-  auto kd = k_draws<4, 2>;
+  auto kd = wide ? k_draws<8, 2, kDrawMTWalk, 2> : k_draws<4, 2>;
+  const int nwd = wide ? 8 : 4;
   if (ensure_dyn_lds((const void*)kd, lds) != TCI_OK) return TCI_EHIP;
   const int npass = draws_passes(p.walk != 0);
-  const int64_t per_wg = (int64_t)kDrawSteps * npass;  // <= the workgroup's threads (scalar draws)
+  const int64_t per_wg = (int64_t)8 * (wide ? kDrawMTWalk : kDrawMT) * npass;  // <= the threads (scalar draws)
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
-  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(64 * 4), lds, stream, st, p, s_begin, s_end, npass);
+  hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(64 * nwd), lds, stream, st, p, s_begin, s_end, npass);
   if (p.walk)
     hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, stream, st, p,
                        kp, s_begin, s_end, with_records);
@@ -2536,7 +2548,7 @@ int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
   // TestData adaptation against 4 waves x 12 tiles (r03af; 28 VGPRs spilled, still faster)
   if (p.pmax <= 16 * 9) return launch_adapt_mfma<8, 9, 6, 4>(st, p, stream);
   // P <= 208: 8 waves x 12 tiles (16 waves x 6 tiles measured slower)
-  if (p.pmax <= 16 * 13) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
+  if (p.pmax <= 16 * 13 && p.pmax <= TCI_ADAPT_GT_FROM) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
   const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax);
   if (ensure_dyn_lds((const void*)k_adapt_gt, lds) != TCI_OK) return TCI_EHIP;
   hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.n_chains), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);

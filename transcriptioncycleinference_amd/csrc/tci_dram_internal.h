@@ -19,6 +19,13 @@ constexpr int64_t dram_cov_stride(int64_t ld) {
   return ld * ld > (ld + 15) / 16 * ((ld + 15) / 16 + 1) / 2 * 256 ? ld * ld : (ld + 15) / 16 * ((ld + 15) / 16 + 1) / 2 * 256;
 }
 
+#ifndef TCI_DRAWS_GIB
+#define TCI_DRAWS_GIB 2  // the fused engine's draws buffer: at most this many GiB (sets the chunk length)
+#endif
+#ifndef TCI_ADAPT_GT_FROM
+#define TCI_ADAPT_GT_FROM 208  // rows longer than this adapt with k_adapt_gt (tiles in global memory)
+#endif
+
 struct DramState {
   int64_t n_chains;
   int64_t ld;
