@@ -1378,7 +1378,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       const double* x1 = X[2 * h];
       const double* x2 = X[2 * h + 1];
       const double ssA = x1[0], ssB = x2[0];
-      const double prA = x1[2] != 0.0 ? x1[1] : 0.0, prB = x2[2] != 0.0 ? x2[1] : 0.0;
+      const double prA = x1[1], prB = x2[1];  // 0.0 for a candidate out of bounds (never evaluated)
       const double ipu = xip[par][h];
       // one expression, per-lane operands: a12 (k3 = 0), a32 (k3 = 1), l2 (k3 = 2)
       const double eA = k3 == 2 ? ssB : ssA, eB = k3 == 1 ? ssB : ss;
@@ -1413,7 +1413,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 #pragma unroll
         for (int k = 0; k < NJ; ++k) th[k] = yb[lane + 64 * k];
         ss = acc ? x1[0] : x2[0];
-        prior = acc ? (inb1 ? x1[1] : 0.0) : (inb2 ? x2[1] : 0.0);
+        prior = acc ? x1[1] : x2[1];  // an accepted candidate was in bounds
         nacc += 1;
         break;  // step s + hh + 1 must be re-proposed around the new state
       }
