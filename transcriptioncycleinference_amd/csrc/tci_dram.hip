@@ -1898,14 +1898,65 @@ __device__ __forceinline__ void chol16_finish(double (&a)[4], double* dpiv, doub
 // Instances: NW waves per workgroup (one chain), MAXT = max tiles per dimension, kAdOwn output tiles
 // per wave (MAXT (MAXT + 1) / 2 <= NW kAdOwn): <8, 9, 6> for P <= 144 (two chains per CU at 128
 // VGPRs), <8, 13, 12> for P <= 208 (configs 4/5: 200 points, P = 207; one chain per CU).
+// The runs of equal rows among a window's nb rows (k_adapt_mfma, k_adapt_gt): a rejected step
+// repeats the row before it, which adds the same outer product to the scatter again, so the
+// scatter runs once per run, weighted by its length -- about 1 + 100 x the acceptance rate of the
+// 100 rows; the same sum in exact arithmetic, rounded differently from row-by-row sums (and the
+// same in every engine). Wave w of NW compares rows w, w + NW, .. with their predecessors (any
+// entry unequal, NaN included: a new run), RU rows' loads in flight together; wave 0 then lists
+// the run starts in row order. rs[0..m) = start rows, rs[m] = nb; rf: nb ints of LDS scratch.
+template <int NW, int NJA, int RU>
+__device__ int window_runs(const double* win, int64_t ld, int P, int nb, int* rs, int* rf, int* nrun) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  for (int r0 = w; r0 < nb; r0 += RU * NW) {  // uniform per wave
+    double a[RU][NJA], b[RU][NJA];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int r = min(r0 + u * NW, nb - 1), rp = max(r - 1, 0);
+#pragma unroll
+      for (int k = 0; k < NJA; ++k) {
+        const int j = min(lane + 64 * k, P - 1);
+        a[u][k] = win[(int64_t)r * ld + j];
+        b[u][k] = win[(int64_t)rp * ld + j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int r = r0 + u * NW;
+      bool d = r == 0;
+#pragma unroll
+      for (int k = 0; k < NJA; ++k) d = d || !(a[u][k] == b[u][k]);
+      const bool any = wave_ballot(d) != 0;
+      if (lane == 0 && r < nb) rf[r] = any ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  if (w == 0) {  // run starts in row order (a ballot prefix per 64 rows)
+    int m = 0;
+    for (int r0 = 0; r0 < nb; r0 += 64) {
+      const int r = r0 + lane;
+      const bool f = r < nb && rf[r] != 0;
+      const uint64_t bal = wave_ballot(f);
+      if (f) rs[m + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = r;
+      m += __builtin_popcountll(bal);
+    }
+    if (lane == 0) {
+      rs[m] = nb;
+      *nrun = m;
+    }
+  }
+  __syncthreads();
+  return *nrun;
+}
+
 #ifndef TCI_AD_RB
 #define TCI_AD_RB 16
 #endif
-constexpr int kAdRB = TCI_AD_RB;  // window rows per LDS batch
-__host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P) {
+constexpr int kAdRB = TCI_AD_RB;  // window runs per LDS batch
+__host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P, int64_t nb) {
   const int64_t NT = (P + 15) / 16, LX = 16 * NT;
-  const int64_t shared = kAdRB * LX > 2 * NT * 256 ? kAdRB * LX : 2 * NT * 256;  // X | panel buffers
-  return (shared + 2 * LX) * 8;
+  const int64_t shared = 2 * kAdRB * LX > 2 * NT * 256 ? 2 * kAdRB * LX : 2 * NT * 256;  // X, Xw | panel buffers
+  return (shared + 2 * LX) * 8 + ((2 * nb + 2) * 4 + 7) / 8 * 8;  // + the run starts and flags
 }
 
 template <int NW, int MAXT, int kAdOwn, int WPE = (NW <= 8 ? 2 : NW / 4)>  // kAdOwn: output tiles per wave (a
@@ -1920,7 +1971,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   constexpr int kAdMG = kAdOwn <= 6 ? 3 : 6;
   static_assert(kAdOwn % kAdMG == 0, "owned tiles come in whole merge groups");
   extern __shared__ __attribute__((aligned(16))) double dyn[];
-  __shared__ int fail;
+  __shared__ int fail, nrun;
   __shared__ double rdg[16];  // 1 / U[k][k] of the current diagonal tile
   const int t = threadIdx.x, lane = t & 63;  // lane-derived tile indices: lane_idx<kFresh>() where used
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -1930,8 +1981,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const int64_t ld = st.ld;
   const int P = st.npar[c];
   const int NT = (P + 15) >> 4, LX = 16 * NT, T = NT * (NT + 1) / 2;
-  const int shared = max(kAdRB * LX, 2 * NT * 256);
+  const int shared = max(2 * kAdRB * LX, 2 * NT * 256);
   double* X = dyn;                // scatter: a batch of centred window rows [kAdRB][LX]
+  double* Xw = dyn + kAdRB * LX;  //   and the same rows times their run lengths
   double* Pb = dyn;               // Cholesky: panel buffers [2][NT][256] (aliases X)
   double* mb = dyn + shared;      // batch mean
   double* mo = mb + LX;           // old mean
@@ -1939,6 +1991,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   double* mu = st.cmean + c * ld;
   const int nb = (TCI_ADAPT_ABLATE & 2) ? 0 : (int)p.adaptint;
   const double* win = st.window + c * p.win * ld;
+  int* rs = (int*)(mo + LX);  // [nb + 1] the window's runs of equal rows: start rows, then nb
+  int* rf = rs + nb + 1;      // [nb] 1 where a run starts
   uint64_t aph[6] = {0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
 #define TCI_APHASE(k) \
   if (TCI_ADAPT_PROFILE) { a1 = stamp(); aph[k] += a1 - a0; a0 = a1; }
@@ -1963,39 +2017,45 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
     stj[o] = ti + k;
   }
   const int nown = (T - w + NW - 1) / NW;  // valid slots
-  // ---- scatter of the centred rows on MFMA; batch r0 + kAdRB is loaded while r0 is multiplied
+  // ---- the window's runs of equal rows (window_runs)
+  const int M = window_runs<NW, (16 * MAXT + 63) / 64, 4>(win, ld, P, nb, rs, rf, &nrun);
+  // ---- scatter of the centred runs on MFMA: sum over runs of len * d d' (A operand: the rows
+  //      times their lengths, B: the rows); batch m0 + kAdRB is loaded while m0 is multiplied
   f64x4 acc[kAdOwn];
 #pragma unroll
   for (int o = 0; o < kAdOwn; ++o) acc[o] = f64x4{0.0, 0.0, 0.0, 0.0};
   constexpr int kPer = (kAdRB * 16 * kAdM + NTH - 1) / NTH;
   double v[kPer];
-  auto load_batch = [&](int r0) {
-    const int n = min(kAdRB, nb - r0);
+  auto load_batch = [&](int m0) {
+    const int n = min(kAdRB, M - m0);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int e = t + u * NTH, r = e / LX, j = e - r * LX;
-      v[u] = (e < kAdRB * LX && r < n && j < P) ? win[(int64_t)(r0 + r) * ld + j] : 0.0;
+      v[u] = (e < kAdRB * LX && r < n && j < P) ? win[(int64_t)rs[m0 + r] * ld + j] : 0.0;
     }
   };
-  if (nb > 0) load_batch(0);
-  __syncthreads();  // mb
-  for (int r0 = 0; r0 < nb; r0 += kAdRB) {
-    const int n = min(kAdRB, nb - r0);
+  if (M > 0) load_batch(0);
+  for (int m0 = 0; m0 < M; m0 += kAdRB) {
+    const int n = min(kAdRB, M - m0);
 #pragma unroll
     for (int u = 0; u < kPer; ++u) {
       const int e = t + u * NTH, r = e / LX, j = e - r * LX;
-      if (e < kAdRB * LX) X[e] = (r < n && j < P) ? v[u] - mb[j] : 0.0;
+      if (e < kAdRB * LX) {
+        const double d = (r < n && j < P) ? v[u] - mb[j] : 0.0;
+        X[e] = d;
+        Xw[e] = r < n ? (double)(rs[m0 + r + 1] - rs[m0 + r]) * d : 0.0;
+      }
     }
     __syncthreads();
-    if (r0 + kAdRB < nb) load_batch(r0 + kAdRB);
+    if (m0 + kAdRB < M) load_batch(m0 + kAdRB);
     const int lnx = lane_idx<kFresh>();
     for (int k0 = 0; k0 < n; k0 += 4) {
-      const double* xr = X + (k0 + (lnx >> 4)) * LX + (lnx & 15);
+      const int ro = (k0 + (lnx >> 4)) * LX + (lnx & 15);
       double xa[kAdOwn], xb[kAdOwn];
 #pragma unroll
       for (int o = 0; o < kAdOwn; ++o) {
-        xa[o] = xr[16 * sti[o]];
-        xb[o] = xr[16 * stj[o]];
+        xa[o] = Xw[ro + 16 * sti[o]];
+        xb[o] = X[ro + 16 * stj[o]];
       }
 #pragma unroll
       for (int o = 0; o < kAdOwn; ++o) acc[o] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[o], xb[o], acc[o], 0, 0, 0);
@@ -2208,9 +2268,9 @@ __host__ __device__ inline int gt_rows(int64_t P) {  // window rows per LDS batc
   const int64_t rb = (96 * 1024 / 8 - 2 * LX) / LX;
   return (int)std::min<int64_t>(16, std::max<int64_t>(4, rb & ~(int64_t)3));
 }
-__host__ __device__ inline int64_t adapt_gt_lds_bytes(int64_t P) {
+__host__ __device__ inline int64_t adapt_gt_lds_bytes(int64_t P, int64_t nb) {
   const int64_t LX = (P + 15) / 16 * 16;
-  return ((int64_t)gt_rows(P) * LX + 2 * LX) * 8;
+  return ((int64_t)gt_rows(P) * LX + 2 * LX) * 8 + ((2 * nb + 2) * 4 + 7) / 8 * 8;  // + the window's runs
 }
 // tile k of the row-major upper triangle of an n x n tile grid starting at tile row r0 -> (ti, tj)
 __device__ __forceinline__ void tri_tile(int k, int n, int r0, int& ti, int& tj) {
@@ -2227,7 +2287,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
                                                                                                     DramParams p) {
   constexpr int NW = kGtWaves, NTH = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) double dyn[];
-  __shared__ int fail;
+  __shared__ int fail, nrun;
   __shared__ double rdg[16];
   __shared__ double Dt[256];  // U of the current panel's diagonal tile
   const int t = threadIdx.x, lane = t & 63;
@@ -2250,6 +2310,8 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
   auto tile = [&](int ti, int tj) { return Wt + ((int64_t)ti * NT + tj) * 256; };
   const int nb = (int)p.adaptint;
   const double* win = st.window + c * p.win * ld;
+  int* rs = (int*)(mo + LX);  // [nb + 1] the window's runs: start rows, then nb
+  int* rf = rs + nb + 1;      // [nb] scratch
   // TCI_ADAPT_PROFILE: thread 0's s_memtime cycles per phase: scatter, merge, diagonal tiles,
   // panel solves, trailing updates, R store
   uint64_t aph[6] = {0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
@@ -2262,7 +2324,9 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
   const double na = st.wsum[c], nn = na + (double)p.adaptint;
   const double fcross = na * (double)p.adaptint / nn;
   const double rn1 = 1.0 / (nn - 1.0);
-  // ---- covupd: scatter of the centred window rows + merge, kGtTiles tiles per wave and pass
+  const int M = window_runs<NW, 9, 1>(win, ld, P, nb, rs, rf, &nrun);  // P <= 576
+  // ---- covupd: scatter of the centred window runs (each row once, times its run length) + merge,
+  //      kGtTiles tiles per wave and pass
   for (int base = 0; base < T; base += NW * kGtTiles) {
     int ti[kGtTiles], tj[kGtTiles];
     bool val[kGtTiles];
@@ -2275,8 +2339,8 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
     f64x4 acc[kGtTiles];
 #pragma unroll
     for (int g = 0; g < kGtTiles; ++g) acc[g] = f64x4{0.0, 0.0, 0.0, 0.0};
-    for (int r0 = 0; r0 < nb; r0 += rb) {
-      const int n = min(rb, nb - r0);
+    for (int r0 = 0; r0 < M; r0 += rb) {
+      const int n = min(rb, M - r0);
       __syncthreads();  // the previous batch is consumed (and mb is written, first time)
       // the batch's window entries, kGtPer loads in flight per thread before their LDS stores (a
       // plain strided loop waited for each load in turn)
@@ -2285,7 +2349,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
         for (int u = 0; u < kGtPer; ++u) {
           const int e = e0 + u * NTH, r = e / LX, j = e - r * LX;
-          v[u] = (e < rb * LX && r < n && j < P) ? win[(int64_t)(r0 + r) * ld + j] : 0.0;
+          v[u] = (e < rb * LX && r < n && j < P) ? win[(int64_t)rs[r0 + r] * ld + j] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < kGtPer; ++u) {
@@ -2296,9 +2360,12 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
       __syncthreads();
       for (int k0 = 0; k0 < n; k0 += 4) {
         const double* xr = X + (k0 + kq) * LX + row;
+        const int kr = k0 + kq;  // this lane's run: its length weights the A operand (rows past n are 0)
+        const double len = kr < n ? (double)(rs[r0 + kr + 1] - rs[r0 + kr]) : 0.0;
 #pragma unroll
         for (int g = 0; g < kGtTiles; ++g)
-          if (val[g]) acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr[16 * ti[g]], xr[16 * tj[g]], acc[g], 0, 0, 0);
+          if (val[g])
+            acc[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(len * xr[16 * ti[g]], xr[16 * tj[g]], acc[g], 0, 0, 0);
       }
     }
     TCI_GPHASE(0)
@@ -2517,7 +2584,7 @@ int launch_stage(void (*k)(DramState, DramParams), const DramState& st, const Dr
 
 template <int NW, int MAXT, int OWN, int WPE = (NW <= 8 ? 2 : NW / 4)>
 int launch_adapt_mfma(const DramState& st, const DramParams& p, void* stream) {
-  const size_t bytes = (size_t)adapt_mfma_lds_bytes(p.pmax);
+  const size_t bytes = (size_t)adapt_mfma_lds_bytes(p.pmax, p.adaptint);
   auto k = k_adapt_mfma<NW, MAXT, OWN, WPE>;
   if (ensure_dyn_lds((const void*)k, bytes) != TCI_OK) return TCI_EHIP;
   hipLaunchKernelGGL(k, chain_grid(st.n_chains), dim3(64 * NW), bytes, (hipStream_t)stream, st, p);
@@ -2549,7 +2616,7 @@ int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
   if (p.pmax <= 16 * 9) return launch_adapt_mfma<8, 9, 6, 4>(st, p, stream);
   // P <= 208: 8 waves x 12 tiles (16 waves x 6 tiles measured slower)
   if (p.pmax <= 16 * 13 && p.pmax <= TCI_ADAPT_GT_FROM) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
-  const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax);
+  const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax, p.adaptint);
   if (ensure_dyn_lds((const void*)k_adapt_gt, lds) != TCI_OK) return TCI_EHIP;
   hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.n_chains), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);
   return finish();
