@@ -809,10 +809,9 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
 #endif
 constexpr int kDrawsPF = 2;               // R values prefetched this many k-steps ahead (mfma_zr PF)
 constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each), 4-wave workgroups
-constexpr int kDrawSteps = 8 * kDrawMT;   // steps per pass (2 rows per step)
 enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
 
-// Dynamic LDS of k_draws: one pass's normals (2 x kDrawSteps rows of stride L). The chain's packed
+// Dynamic LDS of k_draws: one pass's normals (2 x 8 x MT rows of stride L). The chain's packed
 // FP64 R is read from global memory (L2) with a kDrawsPF-deep prefetch: staging it in LDS beside the
 // normals (74 KB at P = 136) left one workgroup per CU, and that layout took 144 us per TestData
 // chunk against 105 us with R from L2 and four 35 KB workgroups per CU (r03n/r03o).
