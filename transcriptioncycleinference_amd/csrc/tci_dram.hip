@@ -826,7 +826,10 @@ __host__ __device__ inline bool draws_walk_wide(int64_t L) { return draws_lds_by
 // Passes per workgroup: every workgroup reads the chain's R once per pass. FUSED (a few hundred
 // chains): 2 (1: 108.8, 2: 104.7, 4: 123.7 us per TestData chunk); WALK (thousands of chains, P =
 // 207): 4, fewer and longer workgroups reading R fewer times.
-__host__ __device__ inline int draws_passes(bool walk) { return walk ? 4 : 2; }
+#ifndef TCI_DRAWS_NPASS
+#define TCI_DRAWS_NPASS 1  // fused engine: passes per k_draws workgroup (WALK: 4); 2: 80.4 vs 77.9 us (r04np)
+#endif
+__host__ __device__ inline int draws_passes(bool walk) { return walk ? 4 : TCI_DRAWS_NPASS; }
 
 // NWD waves per workgroup, CT column tiles per wave and MFMA call (launch_chain_t: 4 and 2); longer
 // rows loop over calls. The wave count and CT only move column tiles between waves and calls: same
