@@ -829,7 +829,10 @@ __host__ __device__ inline bool draws_walk_wide(int64_t L) { return draws_lds_by
 #ifndef TCI_DRAWS_NPASS
 #define TCI_DRAWS_NPASS 1  // fused engine: passes per k_draws workgroup (WALK: 4); 2: 80.4 vs 77.9 us (r04np)
 #endif
-__host__ __device__ inline int draws_passes(bool walk) { return walk ? 4 : TCI_DRAWS_NPASS; }
+#ifndef TCI_DRAWS_NPASS_WALK
+#define TCI_DRAWS_NPASS_WALK 4
+#endif
+__host__ __device__ inline int draws_passes(bool walk) { return walk ? TCI_DRAWS_NPASS_WALK : TCI_DRAWS_NPASS; }
 
 // NWD waves per workgroup, CT column tiles per wave and MFMA call (launch_chain_t: 4 and 2); longer
 // rows loop over calls. The wave count and CT only move column tiles between waves and calls: same
