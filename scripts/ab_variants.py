@@ -60,7 +60,7 @@ def build(names, jobs=4):
         list(ex.map(lambda n: build_library(out=os.path.join(OUT, f"libtci_{n}.so"), defines=VARIANTS[n]), todo))
 
 
-def run(names, rounds, launches, proposals):
+def run(names, rounds, launches, proposals, distinct=1):
     import torch
 
     import bench
@@ -70,6 +70,9 @@ def run(names, rounds, launches, proposals):
     theta, cid, active = bench.proposal_batch(cells, proposals, seed=20201028)
     dev = torch.device("cuda", 0)
     th_d = torch.from_numpy(theta).to(dev)
+    # bench-like: launches cycle through `distinct` resident batches (batch 0 is the checked one)
+    th_all = [th_d] + [torch.from_numpy(bench.proposal_batch(cells, proposals, seed=20201028 + i)[0]).to(dev)
+                       for i in range(1, distinct)]
     cid_d = torch.from_numpy(cid).to(dev)
     act_d = torch.from_numpy(active).to(dev)
     # "main": the in-tree libtci.so (the shipped build)
@@ -80,18 +83,18 @@ def run(names, rounds, launches, proposals):
     for n in names:  # warm + correctness
         lks[n].ss_batch_device(th_d, cid_d, outs[n], act_d, stream=st)
     torch.cuda.synchronize()
-    ref = outs[names[0]].cpu().numpy()
-    act = active.astype(bool)
     times = {n: [] for n in names}
     for _ in range(rounds):
         for n in names:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
-            for _ in range(launches):
-                lks[n].ss_batch_device(th_d, cid_d, outs[n], act_d, stream=st)
+            for i in range(launches):
+                lks[n].ss_batch_device(th_all[i % distinct], cid_d, outs[n], act_d, stream=st)
             e1.record(st)
             torch.cuda.synchronize()
             times[n].append(e0.elapsed_time(e1) / launches * 1e3)
+    ref = outs[names[0]].cpu().numpy()  # every variant's last launch read the same batch
+    act = active.astype(bool)
     res = {}
     for n in names:
         got = outs[n].cpu().numpy()
@@ -120,9 +123,10 @@ if __name__ == "__main__":
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--proposals", type=int, default=256)
+    ap.add_argument("--distinct", type=int, default=1, help="resident batches cycled (bench.py: 8)")
     a = ap.parse_args()
     names = [parse_variant(v) for v in a.variants.split(",")]
     if a.build:
         build(names)
     if a.run:
-        run(names, a.rounds, a.launches, a.proposals)
+        run(names, a.rounds, a.launches, a.proposals, a.distinct)
