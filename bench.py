@@ -236,16 +236,30 @@ def end_to_end(lk, n_steps: int, seed: int, reduce=None):
             "accept_rate_median_rank0": float(np.median(fr.accept_rate))}
 
 
-def synthetic_config_cells(cfg: int, rank: int, world: int, device_index: int, n_points: int = 200):
-    """this rank's shard of the 10,000 synthetic cells x 200 points
-    (data seed 20201028 + rank) and the construct (config 5: 2 segments per dye, 3x length)."""
+CONFIG_SHARDS = 8            # the 10,000 synthetic cells are 8 shards of 1,250
+CONFIG_SHARD_CELLS = 1250
+
+
+def config_shards(rank: int, world: int, n_shards: int = CONFIG_SHARDS) -> range:
+    """The shards rank r of N builds and fits: a contiguous range of the fixed shards (every shard
+    once over the ranks; with N > 8 some ranks get none). The dataset is the same at every N."""
+    return range(rank * n_shards // world, (rank + 1) * n_shards // world)
+
+
+def synthetic_config_cells(cfg: int, rank: int, world: int, device_index: int, n_points: int = 200,
+                           shard_cells: int = CONFIG_SHARD_CELLS, n_shards: int = CONFIG_SHARDS):
+    """this rank's shards of the 10,000 synthetic cells x 200 points
+    (shard s: 1,250 cells from data seed 20201028 + s, independent of the GPU count) and the construct
+    (config 5: 2 segments per dye, 3x length). Returns (cells, truth, construct, n_total, n_points,
+    first cell, end cell) with the rank's cells at dataset-wide indices [first, end)."""
     from transcriptioncycleinference_amd import Likelihood, from_lists
     from transcriptioncycleinference_amd.construct import builtin_construct, long_two_loop_construct
     from transcriptioncycleinference_amd.data import synthetic_cells
 
     construct = builtin_construct(CONSTRUCT) if cfg == 4 else long_two_loop_construct()
-    n_total = 10000
-    lo, hi = rank * n_total // world, (rank + 1) * n_total // world
+    n_total = shard_cells * n_shards
+    mine = config_shards(rank, world, n_shards)
+    lo, hi = mine.start * shard_cells, mine.stop * shard_cells
 
     def fwd(times, theta):
         nan = [np.full(len(t), np.nan) for t in times]
@@ -253,16 +267,24 @@ def synthetic_config_cells(cfg: int, rank: int, world: int, device_index: int, n
         with Likelihood(tab, construct, device=device_index) as L:
             return L.forward(theta, np.arange(len(times), dtype=np.int32), grid="interp")
 
-    cells, truth = synthetic_cells(hi - lo, n_points, 20201028 + rank, fwd)
-    return cells, truth, construct, n_total, n_points, lo, hi
+    parts, truths = [], []
+    for s in mine:
+        c, th = synthetic_cells(shard_cells, n_points, 20201028 + s, fwd)
+        parts.append(c)
+        truths.append(th)
+    if not parts:
+        return from_lists([], "synthetic-empty"), np.zeros((0, 7 + n_points)), construct, n_total, n_points, lo, hi
+    cells = from_lists([p.cell(k) for p in parts for k in range(p.n_cells)],
+                       f"synthetic-{n_total}x{n_points}-shards{mine.start}-{mine.stop - 1}")
+    return cells, np.concatenate(truths), construct, n_total, n_points, lo, hi
 
 
 def synthetic_kernel(cfg: int, rank: int, world: int, device_index: int, proposals: int, warmup: int, steps: int,
                      reduce):
-    """SURVEY.md §8(d) configs 4/5 in kernel mode: 10,000 synthetic cells x 200 points, sharded
-    10,000/world cells per GPU (data seed 20201028 + rank), `proposals` Gaussian proposals per cell
-    around the ground truth with the reference's J0 variances (bounds-rejected rows inactive, not
-    counted). Config 5 runs the 2-segment, 3x-length construct. Strong scaling: the total is fixed."""
+    """SURVEY.md §8(d) configs 4/5 in kernel mode: 10,000 synthetic cells x 200 points in 8 fixed
+    shards, this rank's shards on its GPU, `proposals` Gaussian proposals per cell around the ground
+    truth with the reference's J0 variances (proposal seed 7 + shard; bounds-rejected rows inactive,
+    not counted). Config 5 runs the 2-segment, 3x-length construct. Strong scaling: the total is fixed."""
     import torch
 
     from transcriptioncycleinference_amd import Likelihood
@@ -270,85 +292,111 @@ def synthetic_kernel(cfg: int, rank: int, world: int, device_index: int, proposa
 
     cells, truth, construct, n_total, n_points, lo, hi = synthetic_config_cells(cfg, rank, world, device_index)
     C, ld = truth.shape
-    rng = np.random.default_rng(7 + rank)
-    cid = np.repeat(np.arange(C, dtype=np.int32), proposals)
-    dtl = np.array([cells.cell(c)[0][-1] - cells.cell(c)[0][-2] for c in range(C)])
-    sd = np.sqrt(np.concatenate([np.tile([0.05, 0.1, 0.0, 1.0, 1.0, 0.05, 0.5], (C, 1)), np.full((C, ld - 7), 0.5)], 1))
-    sd[:, 2] = np.sqrt(dtl)
-    theta = truth[cid] + rng.normal(0.0, 1.0, (len(cid), ld)) * sd[cid]
-    active = np.all((theta[:, :7] >= LOWER) & (theta[:, :7] <= UPPER), axis=1)
-    active &= np.all((theta[:, 7:] >= DR_BOUNDS[0]) & (theta[:, 7:] <= DR_BOUNDS[1]), axis=1)
-    active = active.astype(np.uint8)
-    dev = torch.device("cuda", device_index)
-    lk = Likelihood(cells, construct, device=device_index)
-    th_d, cid_d = torch.from_numpy(theta).to(dev), torch.from_numpy(cid).to(dev)
-    act_d, out_d = torch.from_numpy(active).to(dev), torch.empty(len(cid), dtype=torch.float64, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    for _ in range(warmup):
-        lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=stream)
-    torch.cuda.synchronize(dev)
+    out = {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points in {CONFIG_SHARDS} shards, "
+                       f"{proposals} proposals/cell, construct {construct.name}, {hi - lo} cells on rank 0",
+           "unit": "SS evals/s", "scaling": "strong"}
+    n_act, kernel_ms, alg, ok, rpl = 0, 0.0, 0, True, None
+    if C:
+        cid = np.repeat(np.arange(C, dtype=np.int32), proposals)
+        theta = np.empty((len(cid), ld))
+        for k, s in enumerate(config_shards(rank, world)):  # proposals keyed by shard: N-independent
+            rng = np.random.default_rng(7 + s)
+            rows = slice(k * CONFIG_SHARD_CELLS * proposals, (k + 1) * CONFIG_SHARD_CELLS * proposals)
+            theta[rows] = rng.normal(0.0, 1.0, (CONFIG_SHARD_CELLS * proposals, ld))
+        dtl = np.array([cells.cell(c)[0][-1] - cells.cell(c)[0][-2] for c in range(C)])
+        sd = np.sqrt(np.concatenate([np.tile([0.05, 0.1, 0.0, 1.0, 1.0, 0.05, 0.5], (C, 1)), np.full((C, ld - 7), 0.5)], 1))
+        sd[:, 2] = np.sqrt(dtl)
+        theta = truth[cid] + theta * sd[cid]
+        active = np.all((theta[:, :7] >= LOWER) & (theta[:, :7] <= UPPER), axis=1)
+        active &= np.all((theta[:, 7:] >= DR_BOUNDS[0]) & (theta[:, 7:] <= DR_BOUNDS[1]), axis=1)
+        active = active.astype(np.uint8)
+        dev = torch.device("cuda", device_index)
+        lk = Likelihood(cells, construct, device=device_index)
+        th_d, cid_d = torch.from_numpy(theta).to(dev), torch.from_numpy(cid).to(dev)
+        act_d, out_d = torch.from_numpy(active).to(dev), torch.empty(len(cid), dtype=torch.float64, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        for _ in range(warmup):
+            lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=stream)
+        torch.cuda.synchronize(dev)
     reduce(0.0, "max")  # barrier
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(steps):
-        lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=stream)
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
+    if C:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
     elapsed = reduce(time.perf_counter() - t0, "max")
-    kernel_ms = e0.elapsed_time(e1) / steps
-    ss = out_d.cpu().numpy()
-    n_act = int(active.sum())
-    alg = algorithmic_bytes(cells, cid, active)
-    out = {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points, {proposals} proposals/cell, "
-                       f"construct {construct.name}, {hi - lo} cells on rank 0",
-           "value": reduce(n_act, "sum") * steps / elapsed, "unit": "SS evals/s", "scaling": "strong",
-           "kernel_ms_rank0": kernel_ms, "rows_per_launch_rank0": len(cid), "in_bounds_rank0": n_act,
-           "hbm_frac_rank0": alg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-           "kernel_rows_per_lane": lk.info["rows_per_lane"],
-           "results_finite": bool(np.all(np.isfinite(ss[active.astype(bool)])))}
-    lk.close()
+    if C:
+        kernel_ms = e0.elapsed_time(e1) / steps
+        ss = out_d.cpu().numpy()
+        n_act = int(active.sum())
+        alg = algorithmic_bytes(cells, cid, active)
+        ok = bool(np.all(np.isfinite(ss[active.astype(bool)])))
+        rpl = lk.info["rows_per_lane"]
+        lk.close()
+        out.update({"rows_per_launch_rank0": len(cid), "in_bounds_rank0": n_act})
+    out.update({"value": reduce(n_act, "sum") * steps / elapsed, "kernel_ms_rank0": kernel_ms,
+                "hbm_frac_rank0": alg / max(kernel_ms * 1e-3, 1e-30) / 1e9 / HBM_PEAK_GBS,
+                "kernel_rows_per_lane": rpl, "results_finite": bool(reduce(0.0 if ok else 1.0, "sum") == 0.0)})
     return out
 
 
 def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_steps: int, reduce,
-                         engine: str = "auto", n_points: int = 200):
-    """SURVEY.md §8(d) configs 4/5 end to end: this rank's shard of the 10,000 synthetic cells
-    fitted by the GPU-resident DRAM (one chain per cell, n_burn = n_steps/20), as
-    `parallel.fit_sharded` runs it minus the results gather. Strong scaling: 10,000 cells in total.
+                         engine: str = "auto", n_points: int = 200, coll_device: str = None):
+    """SURVEY.md §8(d) configs 4/5 end to end, as `parallel.fit_sharded` runs a sharded fit: 10,000
+    synthetic cells in 8 fixed shards, rank r fits its shards (one GPU-resident DRAM chain per cell,
+    n_burn = n_steps/20, chains keyed by the dataset-wide cell index, so the fit is the same at every
+    GPU count), then ONE all-gather of the packed per-cell results (RCCL over xGMI on a multi-GPU node)
+    -- inside the timed region, and timed on its own too. Strong scaling: 10,000 cells in total.
     BASELINE configs 4/5 name n_steps = 200000 (the default); a smaller n_steps is labelled a sample."""
     from transcriptioncycleinference_amd import Likelihood
-    from transcriptioncycleinference_amd.mcmc import DramOptions, fit
+    from transcriptioncycleinference_amd.mcmc import DramOptions
+    from transcriptioncycleinference_amd.parallel import fit_sharded
 
     cells, _, construct, n_total, n_points, lo, hi = synthetic_config_cells(cfg, rank, world, device_index, n_points)
     with Likelihood(cells, construct, device=device_index) as lk:
         reduce(0.0, "max")  # barrier
         t0 = time.perf_counter()
-        fr = fit(lk, n_steps=n_steps, n_burn=max(1, n_steps // 20), seed=cfg, opts=DramOptions(engine=engine))
+        fr = fit_sharded(lk, device=coll_device, cell_offset=lo, n_steps=n_steps, n_burn=max(1, n_steps // 20),
+                         seed=cfg, opts=DramOptions(engine=engine))
         wall = reduce(time.perf_counter() - t0, "max")
-        # output checks (untimed): every chain's summaries and final state finite and in bounds, and
-        # the GPU SS of a sample of final states, which the cpu_baseline leg re-evaluates on the oracle
-        fin = fr.final_theta
-        ok = bool(np.all([np.isfinite(r["mean_v"]) and np.isfinite(r["mean_sigma"]) and np.all(np.isfinite(r["mean_dR"]))
-                          for r in fr.MCMCresults]))
-        lens = cells.lengths[fr.cell_index]
-        ok = ok and all(np.all(np.isfinite(fin[k, :7 + n])) for k, n in enumerate(lens))
-        sample = np.linspace(0, len(fr.cell_index) - 1, min(256, len(fr.cell_index))).astype(np.int64)
-        s_theta = np.ascontiguousarray(fin[sample])
-        s_cid = fr.cell_index[sample].astype(np.int32)
-        s_ss = lk.ss_batch(s_theta, s_cid)
-        ok = ok and bool(np.all(np.isfinite(s_ss)))
-    dev_s, evals = reduce(fr.elapsed_ms * 1e-3, "max"), int(reduce(fr.n_evals, "sum"))
-    out = {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points, construct {construct.name}, "
-                       f"{hi - lo} chains on rank 0, {n_steps} steps"
-                       + ("" if n_steps >= 200000 else " (bounded sample of the configured 200k)"),
-           "n_steps": n_steps, "engine": engine, "chains": int(reduce(len(fr.MCMCresults), "sum")), "device_s": dev_s,
+        # output checks (untimed): every gathered cell's summaries finite, every local final state finite,
+        # and the GPU SS of a sample of this rank's final states, which the cpu_baseline leg re-evaluates
+        # on the oracle
+        ok = len(fr.MCMCresults) == n_total and [r["cell_index"] for r in fr.MCMCresults] == list(range(1, n_total + 1))
+        ok = ok and bool(np.all([np.isfinite(r["mean_v"]) and np.isfinite(r["mean_sigma"]) and
+                                 np.all(np.isfinite(r["mean_dR"])) for r in fr.MCMCresults]))
+        loc = fr.local
+        s_theta, s_cid, s_ss = np.zeros((0, 7 + n_points)), np.zeros(0, np.int32), np.zeros(0)
+        if loc is not None:
+            fin = loc.final_theta
+            lens = cells.lengths[loc.cell_index - lo]
+            ok = ok and all(np.all(np.isfinite(fin[k, :7 + n])) for k, n in enumerate(lens))
+            sample = np.linspace(0, len(loc.cell_index) - 1, min(256, len(loc.cell_index))).astype(np.int64)
+            s_theta = np.ascontiguousarray(fin[sample])
+            s_cid = (loc.cell_index[sample] - lo).astype(np.int32)
+            s_ss = lk.ss_batch(s_theta, s_cid)
+            ok = ok and bool(np.all(np.isfinite(s_ss)))
+    dev_s = fr.elapsed_ms * 1e-3     # max over ranks (fit_sharded)
+    evals = int(fr.n_evals)          # summed over ranks (fit_sharded)
+    gather_s = reduce(fr.gather_s, "max")
+    acc = float(np.median([r for r in fr.accept_rate])) if len(fr.accept_rate) else float("nan")
+    out = {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points in {CONFIG_SHARDS} shards "
+                       f"(seed 20201028 + shard), construct {construct.name}, {hi - lo} chains on rank 0, "
+                       f"{n_steps} steps, results all-gathered" + ("" if n_steps >= 200000 else
+                                                                    " (bounded sample of the configured 200k)"),
+           "n_steps": n_steps, "engine": engine, "chains": len(fr.MCMCresults), "device_s": dev_s,
            "wall_s": wall, "ssfun_evals": evals, "value": evals / wall, "unit": "SS evals/s (wall time)",
            "value_basis": "wall",
            "scaling": "strong", "us_per_step": wall * 1e6 / max(n_steps - 1, 1),
            "device_value": evals / dev_s, "device_us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
-           "accept_rate_median_rank0": float(np.median(fr.accept_rate)),
-           "outputs_finite_rank0": ok}
+           "gather_s": gather_s, "gather_bytes_per_rank": fr.gather_bytes,
+           "gather_collective": "RCCL all-gather" if coll_device and str(coll_device).startswith("cuda") and world > 1
+           else ("gloo all-gather" if world > 1 else "none (one rank)"),
+           "accept_rate_median": acc,
+           "outputs_finite": bool(reduce(0.0 if ok else 1.0, "sum") == 0.0)}
     spot = {"cells": cells, "construct": construct, "theta": s_theta, "cid": s_cid, "ss_gpu": s_ss}
     return out, spot
 
@@ -734,7 +782,8 @@ def main():
                                                           max(args.steps, 20), reduce)
             if args.synth_dram_steps > 1:
                 res[f"config{cfg}_dram"], spots[cfg] = synthetic_end_to_end(cfg, rank, world, device_index,
-                                                                            args.synth_dram_steps, reduce)
+                                                                            args.synth_dram_steps, reduce,
+                                                                            coll_device=str(coll_dev))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cells, theta_h, rounds_cid(cells, args.proposals), act_h, args.cpu_seconds)
         res["cpu_fit_config1"] = cpu_fit_config1(lk)

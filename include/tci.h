@@ -177,7 +177,10 @@ typedef struct {
 #define TCI_DRAM_BATCHED 2
 #define TCI_DRAM_WALK 3
 
-/* Host buffers filled by tci_dram_run (any may be NULL). Per-chain vectors have stride ld. */
+/* Host buffers filled by tci_dram_run (any may be NULL). Per-chain vectors have stride ld.
+ * Padding (entries j >= P = 7 + N of a chain whose row is shorter than ld): mean and std are NaN
+ * (also every entry when no row is in the statistics range, stats_from > n_steps); final_theta keeps
+ * theta0's padding unchanged; chain rows and qcov_R are 0 there. */
 typedef struct {
   double* mean;         /* mean(chain(stats_from:end, :)) (:286-301) */
   double* std;          /* std(chain(stats_from:end, :), 1) */

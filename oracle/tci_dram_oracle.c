@@ -401,11 +401,16 @@ static int run_chain(const int64_t *offsets, const double *t, const double *ms2,
   }
   if (rc == 0) {
     for (int j = 0; j < P; ++j) {
-      out->mean[c * ld + j] = w.smean[j];
-      out->std[c * ld + j] = ns > 0 ? sqrt(w.sm2[j] / (double)ns) : 0.0;
+      out->mean[c * ld + j] = ns > 0 ? w.smean[j] : NAN;
+      out->std[c * ld + j] = ns > 0 ? sqrt(w.sm2[j] / (double)ns) : NAN;
       out->final_theta[c * ld + j] = th[j];
     }
-    for (int j = P; j < ld; ++j) out->mean[c * ld + j] = out->std[c * ld + j] = out->final_theta[c * ld + j] = 0.0;
+    /* padding past the chain's P (include/tci.h, tci_dram_outputs): mean/std NaN, final_theta
+     * the caller's theta0 padding, unchanged */
+    for (int j = P; j < ld; ++j) {
+      out->mean[c * ld + j] = out->std[c * ld + j] = NAN;
+      out->final_theta[c * ld + j] = x0[j];
+    }
     out->sigma_mean[c] = sqrt(s2sum / s2n);
     out->sigma_std[c] = sqrt(qm2 / s2n);
     out->accept_rate[c] = o->n_steps > 1 ? (double)nacc / (double)(o->n_steps - 1) : 0.0;

@@ -125,3 +125,39 @@ def test_gloo_world2_sharded_results_gather_round_trip():
         np.testing.assert_array_equal(pa["simPP7"], pb["simPP7"])
         assert len(pa["t_plot"]) == len(a["mean_dR"])
     np.testing.assert_array_equal(fr.accept_rate, want.accept_rate)
+
+
+def test_config_shards_are_the_same_dataset_at_every_world_size():
+    """bench.py configs 4/5: 10,000 cells as 8 fixed shards of 1,250 (seed
+    20201028 + shard); rank r of N owns a contiguous range of whole shards, so the global dataset --
+    and with chains keyed by dataset-wide cell index, the fit -- does not depend on N."""
+    import bench
+
+    for world in range(1, 11):
+        got = [list(bench.config_shards(r, world)) for r in range(world)]
+        flat = [s for g in got for s in g]
+        assert flat == list(range(bench.CONFIG_SHARDS)), (world, got)
+        sizes = [len(g) for g in got]
+        assert max(sizes) - min(sizes) <= 1
+    assert bench.CONFIG_SHARDS * bench.CONFIG_SHARD_CELLS == 10000
+
+
+def test_unpack_results_of_a_shard_local_rank():
+    """A rank that loaded only its own block of cells (parallel.fit_sharded's cell_offset layout)
+    unpacks the gathered rows of every cell: its own cells get their data columns, the others the
+    simulated rows only."""
+    from transcriptioncycleinference_amd import testdata
+    from transcriptioncycleinference_amd.parallel import pack_results, unpack_results
+
+    cells = testdata()
+    rows = pack_results(_fake_fit(cells, range(299)), int(cells.lengths.max()))
+    block = cells.subset(range(100, 150))
+    fr = unpack_results(rows, block, "x", 0, 0.0, cell_offset=100)
+    assert [r["cell_index"] for r in fr.MCMCresults] == list(range(1, 300))
+    for c, p in enumerate(fr.MCMCplot):
+        n = int(cells.lengths[c])
+        assert len(p["simMS2"]) == n
+        if 100 <= c < 150:
+            np.testing.assert_array_equal(p["t_plot"], cells.cell(c)[0])
+        else:
+            assert len(p["t_plot"]) == 0

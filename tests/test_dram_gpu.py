@@ -7,6 +7,8 @@ reproduced); what is checked instead:
 * determinism per seed, bounds (incl. the hierarchical fixed-v fit), bookkeeping (n_steps=1);
 * recovery of ground truth on synthetic cells; the reference's output structs round-trip.
 """
+import dataclasses
+
 import numpy as np
 import pytest
 
@@ -678,3 +680,181 @@ def test_gpu_chains_follow_the_cpu_restatement(lk, c_oracle, construct, engine):
         np.testing.assert_allclose(g.mean[k, :P], c["mean"][k, :P], rtol=1e-9, atol=1e-9)
         np.testing.assert_allclose(g.std[k, :P], c["std"][k, :P], rtol=1e-7, atol=1e-9)
     assert np.median(g.accept_rate) > 0.02
+
+
+# BASELINE configs 4/5 shapes for the restatement check, and one past the
+# 8-wave adaptation kernel: (chains, points per cell, construct, data seed).
+#   config4: N = 200, P = 207, the built-in construct -- k_adapt_mfma<8, 13>, WALK / FUSED / batched;
+#   config5: N = 200, the two-segment 3x-length construct (BASELINE config 5);
+#   long:    N = 210, P = 217 > 208 -- the generic adaptation kernel k_adapt_gt.
+RESTATEMENT_SHAPES = {
+    "config4": (24, 200, "builtin", 20201028),
+    "config5": (16, 200, "two_segment", 20201029),
+    "long": (8, 210, "builtin", 20201030),
+}
+_restatement_cache = {}
+
+
+def _restatement_case(shape, c_oracle):
+    """Synthetic cells of the shape (SURVEY §8(d) item 4's generator), the reference's per-cell setup
+    (plan_fit) and the CPU restatement's chains -- computed once per shape for every engine."""
+    if shape in _restatement_cache:
+        return _restatement_cache[shape]
+    from transcriptioncycleinference_amd import Likelihood, from_lists
+    from transcriptioncycleinference_amd.construct import builtin_construct, long_two_loop_construct
+    from transcriptioncycleinference_amd.data import synthetic_cells
+    from transcriptioncycleinference_amd.mcmc import DramOptions, plan_fit
+
+    n_cells, n_points, cname, seed = RESTATEMENT_SHAPES[shape]
+    cs = builtin_construct("P2P-MS2v5-LacZ-PP7v4") if cname == "builtin" else long_two_loop_construct()
+
+    def fwd(times, theta):
+        nan = [np.full(len(t), np.nan) for t in times]
+        with Likelihood(from_lists([(t, a, a) for t, a in zip(times, nan)]), cs, device=0) as L:
+            return L.forward(theta, np.arange(len(times), dtype=np.int32), grid="interp")
+
+    cells, _ = synthetic_cells(n_cells, n_points, seed, fwd)
+    plan = plan_fit(cells, list(range(n_cells)), 5)
+    o = DramOptions(n_steps=700, burnintime=300, adaptint=100, stats_from=200, thin=1, seed=91)
+    keys = np.array(plan.cells, np.int64)
+    want = c_oracle.dram_run(cells, cs, np.array(plan.cells, np.int32), plan.x0, plan.lower, plan.upper,
+                             plan.prior_mu, plan.prior_sig, plan.qcov_diag, 1.0, o, keys=keys, want_chain=True,
+                             want_R=True)
+    _restatement_cache[shape] = (cells, cs, plan, o, keys, want)
+    return _restatement_cache[shape]
+
+
+@pytest.mark.parametrize("engine", ["fused", "walk", "batched"])
+@pytest.mark.parametrize("shape", sorted(RESTATEMENT_SHAPES))
+def test_gpu_chains_follow_the_cpu_restatement_at_config_shapes(c_oracle, shape, engine):
+    """As test_gpu_chains_follow_the_cpu_restatement, at the shapes BASELINE configs 4/5 run
+    (TranscriptionCycleMCMC.m:263-273): 700 steps, burn-in scaling at rows 100-300, then four covariance
+    updates (rows 400-700) on the P <= 208 matrix-core adaptation (k_adapt_mfma<8, 13>) or, for P = 217,
+    on k_adapt_gt; every engine. Same accept / reject decision at every step; rows, s2chain, summaries
+    and the final proposal factor R within 1e-9."""
+    from transcriptioncycleinference_amd import Likelihood
+    from transcriptioncycleinference_amd.mcmc import dram_run
+
+    cells, cs, plan, o, keys, c = _restatement_case(shape, c_oracle)
+    o = dataclasses.replace(o, engine=engine)
+    with Likelihood(cells, cs, device=0) as L:
+        g = dram_run(L, np.array(plan.cells, np.int32), plan.x0, plan.lower, plan.upper, plan.prior_mu,
+                     plan.prior_sig, plan.qcov_diag, 1.0, o, chain_keys=keys, want_qcov=True)
+    n = cells.lengths[plan.cells]
+    assert int(7 + n.max()) == {"config4": 207, "config5": 207, "long": 217}[shape]
+    for k in range(len(plan.cells)):
+        P = 7 + int(n[k])
+        G, Cc = g.chain[:, k, :P], c["chain"][:, k, :P]
+        moved_g = np.any(G[1:] != G[:-1], axis=1)
+        moved_c = np.any(Cc[1:] != Cc[:-1], axis=1)
+        np.testing.assert_array_equal(moved_g, moved_c, err_msg=f"{shape} chain {k}: accept/reject decisions differ")
+        np.testing.assert_allclose(G, Cc, rtol=1e-9, atol=1e-9, err_msg=f"{shape} chain {k}")
+        np.testing.assert_allclose(g.s2chain[:, k], c["s2chain"][:, k], rtol=1e-9)
+        assert g.n_evals[k] == c["n_evals"][k]
+        np.testing.assert_allclose(g.mean[k, :P], c["mean"][k, :P], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(g.std[k, :P], c["std"][k, :P], rtol=1e-7, atol=1e-9)
+        np.testing.assert_allclose(g.sigma_mean[k], c["sigma_mean"][k], rtol=1e-9)
+        R, Rc = g.qcov_R[k, :P, :P], c["R"][k, :P, :P]
+        np.testing.assert_allclose(R, Rc, rtol=1e-9, atol=1e-9 * np.abs(Rc).max(), err_msg=f"{shape} chain {k}: R")
+    moved = np.any(g.chain[1:] != g.chain[:-1], axis=2).mean(axis=0)
+    assert np.median(moved) > 0.01, moved
+
+
+def test_output_padding_is_the_documented_contract(c_oracle):
+    """include/tci.h (tci_dram_outputs): past a chain's P, mean/std are NaN, final_theta keeps theta0's
+    padding, chain rows and qcov_R are 0 -- on the GPU and in the CPU restatement alike (two cell
+    lengths in one run, so the shorter chain's rows are padded)."""
+    from transcriptioncycleinference_amd import Likelihood, from_lists
+    from transcriptioncycleinference_amd.mcmc import DramOptions, dram_run, plan_fit
+
+    cells, cs = _restatement_case("config4", c_oracle)[:2]
+    two = from_lists([cells.cell(0), tuple(a[:150] for a in cells.cell(1))])
+    p = plan_fit(two, [0, 1], 5)
+    p.x0[1, 157:] = 3.25                                    # theta0 padding the outputs must keep
+    o = DramOptions(n_steps=250, burnintime=100, adaptint=100, stats_from=50, thin=1, seed=4)
+    with Likelihood(two, cs, device=0) as L:
+        g = dram_run(L, np.array([0, 1], np.int32), p.x0, p.lower, p.upper, p.prior_mu, p.prior_sig, p.qcov_diag,
+                     1.0, o, want_qcov=True)
+    c = c_oracle.dram_run(two, cs, np.array([0, 1], np.int32), p.x0, p.lower, p.upper, p.prior_mu, p.prior_sig,
+                          p.qcov_diag, 1.0, o, want_chain=True, want_R=True)
+    for name, got, want in (("mean", g.mean, c["mean"]), ("std", g.std, c["std"])):
+        assert np.all(np.isnan(got[1, 157:])) and np.all(np.isnan(want[1, 157:])), name
+        assert np.all(np.isfinite(got[:, :157])) and np.all(np.isfinite(got[0])), name
+    np.testing.assert_array_equal(g.final_theta[1, 157:], 3.25)
+    np.testing.assert_array_equal(c["final_theta"][1, 157:], 3.25)
+    assert np.all(g.chain[:, 1, 157:] == 0) and np.all(c["chain"][:, 1, 157:] == 0)
+    assert np.all(g.qcov_R[1, 157:, :] == 0) and np.all(g.qcov_R[1, :, 157:] == 0)
+    assert np.all(c["R"][1, 157:, :] == 0)
+    # no statistics rows at all: every mean / std entry is NaN
+    o.stats_from = 251
+    with Likelihood(two, cs, device=0) as L:
+        g = dram_run(L, np.array([0, 1], np.int32), p.x0, p.lower, p.upper, p.prior_mu, p.prior_sig, p.qcov_diag,
+                     1.0, o)
+    c = c_oracle.dram_run(two, cs, np.array([0, 1], np.int32), p.x0, p.lower, p.upper, p.prior_mu, p.prior_sig,
+                          p.qcov_diag, 1.0, o)
+    assert np.all(np.isnan(g.mean)) and np.all(np.isnan(c["mean"])) and np.all(np.isnan(g.std))
+
+
+def _config_shard_worker(rank, world, port, q, n_shards, shard_cells):
+    """One rank of a config-4-shaped sharded fit: builds ONLY its own shards of the synthetic dataset
+    (bench.synthetic_config_cells: shard s from seed 20201028 + s), fits them with chains keyed by the
+    dataset-wide cell index, then the one all-gather (parallel.fit_sharded, cell_offset layout)."""
+    import os
+
+    import torch.distributed as dist
+
+    import bench
+    from transcriptioncycleinference_amd import Likelihood
+    from transcriptioncycleinference_amd.parallel import fit_sharded, pack_results
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cells, _, cs, n_total, _, lo, hi = bench.synthetic_config_cells(4, rank, world, 0, shard_cells=shard_cells,
+                                                                    n_shards=n_shards)
+    assert cells.n_cells == hi - lo
+    with Likelihood(cells, cs, device=0) as L:
+        fr = fit_sharded(L, cell_offset=lo, n_steps=300, n_burn=150, seed=4)
+    if rank == 0:
+        q.put((pack_results(fr, 200), fr.gather_bytes, fr.n_evals))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_config4_sharded_fit_is_the_same_at_every_world_size():
+    """BASELINE config 4's layout -- fixed shards seeded 20201028 + shard, rank r of N
+    builds only its own shards -- fitted over 2 ranks (gloo, both on this GPU; RCCL on a multi-GPU node)
+    gathers to rows bitwise equal to the one-rank fit of the same shards (4 shards x 48 cells x 200
+    points, 300 steps)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    import bench
+    from transcriptioncycleinference_amd import Likelihood
+    from transcriptioncycleinference_amd.parallel import fit_sharded, pack_results
+
+    n_shards, shard_cells = 4, 48
+    cells, _, cs, n_total, _, lo, hi = bench.synthetic_config_cells(4, 0, 1, 0, shard_cells=shard_cells,
+                                                                    n_shards=n_shards)
+    assert (lo, hi, n_total) == (0, 192, 192)
+    with Likelihood(cells, cs, device=0) as L:
+        one = fit_sharded(L, cell_offset=0, n_steps=300, n_burn=150, seed=4)
+    want = pack_results(one, 200)
+    assert want.shape[0] == 192 and one.gather_bytes == want.nbytes
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_config_shard_worker, args=(r, 2, port, q, n_shards, shard_cells)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, nbytes, n_evals = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(got, want)
+    assert nbytes == want.nbytes and n_evals == one.n_evals
+    assert np.median(got[:, 3]) > 0.01  # accept rates

@@ -69,6 +69,38 @@ def test_s2chain_statistical_pin(cells, chain):
     assert abs(ratio.std() - np.mean(np.sqrt(2 / n2))) < 0.01, ratio.std()  # 0.0911 observed
 
 
+def _gibbs_loglik(s2, ss, n_obs, N0, S20=1.0):
+    """Log-density of the precisions 1/s2 under mcmcstat's sigma^2 Gibbs update with the prior
+    (N0, S20): 1/s2 ~ Gamma((N0 + N)/2, scale 2/(N0 S20 + SS)) (the Jacobian of 1/s2 is the same
+    under every hypothesis, so ratios of this are likelihood ratios of the draws)."""
+    from scipy.special import gammaln
+
+    y = 1.0 / s2
+    k, th = (N0 + n_obs) / 2.0, 2.0 / (N0 * S20 + ss)
+    return float(np.sum((k - 1) * np.log(y) - y / th - gammaln(k) - k * np.log(th)))
+
+
+def test_sigma2_prior_weight_is_pinned_by_the_reference_draws(cells, chain):
+    """mcmcstat's N0 / S20 defaults are not vendored (README.md:5); the reference sets only
+    model.sigma2 = 1 and model.N (TranscriptionCycleMCMC.m:259-260). The 2,691 post-initial s2chain
+    draws of the reference's own run, with the SS of the state they were drawn at, decide between
+    the two candidate priors: the exact Gamma log-likelihood favours N0 = 0 (what the sampler and its
+    restatement implement, oracle/tci_dram_oracle.c) over N0 = 1, S20 = sigma2_0 = 1 by 1.77 nats
+    (likelihood ratio ~5.9), and excludes N0 >= 2 (>= 9 nats). The maximum over N0 on a grid lies in
+    [0, 0.5]. DESIGN.md §5 records the decision."""
+    lens = cells.lengths
+    post = chain["step"] > 0
+    s2, ss = chain["s2"][post], chain["ss"][post]
+    n_obs = 2.0 * lens[chain["cell_id"][post]]          # model.N = length(ydata), NaNs counted (:260)
+    l0 = _gibbs_loglik(s2, ss, n_obs, 0.0)
+    l1 = _gibbs_loglik(s2, ss, n_obs, 1.0)
+    assert l0 - l1 > 1.5, l0 - l1                         # 1.77 observed
+    assert l0 - _gibbs_loglik(s2, ss, n_obs, 2.0) > 8.0   # 9.08 observed
+    grid = np.arange(-2.0, 4.01, 0.25)
+    best = grid[int(np.argmax([_gibbs_loglik(s2, ss, n_obs, g) for g in grid]))]
+    assert 0.0 <= best <= 0.5, best
+
+
 def test_colon_rule_properties():
     v = O.matlab_colon(0.0, 0.1, 1.0)
     assert len(v) == 11 and v[-1] == 1.0 and v[0] == 0.0

@@ -149,8 +149,11 @@ class FitResult:
     accept_rate: np.ndarray
     n_evals: int
     elapsed_ms: float
-    cell_index: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))
+    cell_index: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int64))   # 0-based, dataset-wide
     final_theta: Optional[np.ndarray] = None   # last chain row per fitted cell (padded), mcmcstat results.theta
+    gather_s: float = 0.0                      # parallel.fit_sharded: wall time of the results all-gather
+    gather_bytes: int = 0                      # parallel.fit_sharded: bytes every rank receives in it
+    local: Optional["FitResult"] = None        # parallel.fit_sharded: this rank's own fit (raw chains, final_theta)
 
 
 @dataclass
@@ -188,7 +191,7 @@ class FitPlan:
 
 
 def plan_fit(cl: Cells, ids: Sequence[int], seed: int, ratePriorWidth: float = 50.0, v0=None,
-             approved=None) -> FitPlan:
+             approved=None, cell_offset: int = 0) -> FitPlan:
     """The parfor body's per-cell setup for the cells ``ids`` (host only, no GPU).
 
     ``v0`` (loadPrevious, :193-198) and ``approved`` are per-cell inputs read by cell, never by
@@ -197,23 +200,25 @@ def plan_fit(cl: Cells, ids: Sequence[int], seed: int, ratePriorWidth: float = 5
     carries both. A cell with no previous entry, or an empty/NaN ``mean_v``, is skipped
     (``continue``, :196-198) and so pruned from the outputs (:359-369). ``ApprovedFits`` is the
     previous fit's when v0 came from one (:345-347) unless ``approved`` overrides it; 0 otherwise
-    (:349)."""
+    (:349). ``cell_offset``: the dataset-wide index of ``cl``'s cell 0 (``cl`` holds one shard of a
+    larger dataset): x0 and the per-cell inputs are keyed by the dataset-wide index."""
     rows, keep, appr = [], [], []
     for c in ids:
         c = int(c)
         t = cl.cell(c)[0]
-        prev = _per_cell(v0, c)
+        g = int(cell_offset) + c
+        prev = _per_cell(v0, g)
         a = 0
         if isinstance(prev, PreviousFit):
             a = int(prev.ApprovedFits)
             prev = prev.mean_v
         if v0 is not None and (prev is None or np.size(prev) != 1 or not np.isfinite(float(prev))):
             continue
-        ap = _per_cell(approved, c)
+        ap = _per_cell(approved, g)
         if ap is not None:
             a = int(ap)
         vv = None if v0 is None else float(prev)
-        rows.append(cell_setup(t, np.random.default_rng([int(seed), c]), ratePriorWidth, vv))
+        rows.append(cell_setup(t, np.random.default_rng([int(seed), g]), ratePriorWidth, vv))
         keep.append(c)
         appr.append(a)
     ld = max((len(r[0]) for r in rows), default=7)
@@ -230,7 +235,7 @@ def plan_fit(cl: Cells, ids: Sequence[int], seed: int, ratePriorWidth: float = 5
 
 def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 50.0, seed: int = 0,
         v0=None, approved=None, thin: int = 0, cells: Optional[Sequence[int]] = None,
-        opts: Optional[DramOptions] = None) -> FitResult:
+        opts: Optional[DramOptions] = None, cell_offset: int = 0) -> FitResult:
     """``TranscriptionCycleMCMC`` for one dataset on the GPU: one DRAM chain per cell.
 
     ``lk``: a ``Likelihood`` holding the (truncated) cells. ``v0``: the previous fit of a
@@ -243,10 +248,14 @@ def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 5
 
     Everything random is keyed by the cell index -- x0 by ``default_rng([seed, cell])``, the chain
     by RNG stream ``cell`` -- so fitting a subset of the cells (one GPU's shard,
-    :func:`parallel.fit_sharded`) reproduces those cells' results of the full fit bit for bit."""
+    :func:`parallel.fit_sharded`) reproduces those cells' results of the full fit bit for bit.
+    ``cell_offset``: ``lk`` holds only a contiguous block of a larger dataset, starting at this
+    dataset-wide cell index; keys, x0, per-cell inputs and ``cell_index`` use the dataset-wide index
+    (a rank that loaded only its own shard reproduces the one-GPU fit of the whole dataset)."""
     cl: Cells = lk.cells
     ids = list(range(cl.n_cells)) if cells is None else [int(c) for c in cells]
-    plan = plan_fit(cl, ids, seed, ratePriorWidth, v0, approved)
+    off = int(cell_offset)
+    plan = plan_fit(cl, ids, seed, ratePriorWidth, v0, approved, cell_offset=off)
     keep = plan.cells
     if not keep:
         return FitResult(cl.name, [], [], [], np.zeros(0), 0, 0.0)
@@ -255,7 +264,7 @@ def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 5
     o.n_steps, o.burnintime, o.stats_from, o.thin = int(n_steps), int(n_burn), int(max(n_burn, 1)), int(thin)
     o.seed = int(seed) * 1000003 + 20201028
     res = dram_run(lk, np.array(keep, np.int32), plan.x0, plan.lower, plan.upper, plan.prior_mu, plan.prior_sig,
-                   plan.qcov_diag, 1.0, o, chain_keys=np.array(keep, np.int64))
+                   plan.qcov_diag, 1.0, o, chain_keys=np.array(keep, np.int64) + off)
     # forward model at the means on the raw times (:307-309)
     ms2, pp7 = lk.forward(res.mean, np.array(keep, np.int32), grid="raw")
     results, plots, chains = [], [], []
@@ -269,7 +278,7 @@ def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 5
             r["sigma_" + name] = float(std[THETA_INDEX[name]])
         r["mean_dR"], r["sigma_dR"] = mean[7:].copy(), std[7:].copy()
         r["mean_sigma"], r["sigma_sigma"] = float(res.sigma_mean[k]), float(res.sigma_std[k])
-        r["cell_index"] = c + 1                                               # :343 (1-based)
+        r["cell_index"] = off + c + 1                                         # :343 (1-based)
         r["ApprovedFits"] = plan.approved[k]                                  # :345-350
         results.append({f: r[f] for f in RESULT_FIELDS})
         plots.append({"t_plot": t.copy(), "MS2_plot": m.copy(), "PP7_plot": p.copy(),
@@ -286,7 +295,7 @@ def fit(lk, n_steps: int = 20000, n_burn: int = 10000, ratePriorWidth: float = 5
             ch["s2chain"] = res.s2chain[:, k].copy()  # s2chain is not sliced by n_burn (:323)
         chains.append(ch)
     return FitResult(cl.name, results, plots, chains, res.accept_rate, int(res.n_evals.sum()), res.elapsed_ms,
-                     np.array(keep, np.int64), res.final_theta)
+                     np.array(keep, np.int64) + off, res.final_theta)
 
 
 # ---------------------------------------------------------------------------

@@ -79,8 +79,10 @@ def gather_rows(local: np.ndarray, group=None, device: Optional[str] = None) -> 
     import torch
     import torch.distributed as dist
 
-    world = dist.get_world_size(group)
     local = np.ascontiguousarray(local, np.float64)
+    if not dist.is_available() or not dist.is_initialized():
+        return local.copy()  # one process, no process group: the gather of one rank
+    world = dist.get_world_size(group)
     rows = local.shape[0]
     width = int(np.prod(local.shape[1:])) if local.ndim > 1 else 1
     dev = torch.device(device) if device else torch.device("cpu")
@@ -124,10 +126,14 @@ def pack_results(fr, n_max: int) -> np.ndarray:
     return out
 
 
-def unpack_results(rows: np.ndarray, cells, dataset_name: str, n_evals: int, elapsed_ms: float):
+def unpack_results(rows: np.ndarray, cells, dataset_name: str, n_evals: int, elapsed_ms: float,
+                   cell_offset: int = 0):
     """Inverse of :func:`pack_results` over the gathered rows (any rank order): a ``FitResult``
     sorted by cell, with ``MCMCplot``'s data columns restored from ``cells``. Raw chains are not
-    gathered (``MCMCchain`` entries are empty): they stay on the rank that sampled them."""
+    gathered (``MCMCchain`` entries are empty): they stay on the rank that sampled them.
+    ``cells`` may hold only a contiguous block of the dataset starting at dataset-wide index
+    ``cell_offset`` (a rank that loaded only its shard): cells outside it get empty data columns
+    (``t_plot`` / ``MS2_plot`` / ``PP7_plot``) -- the simulated rows are always there."""
     from .mcmc import FitResult
 
     rows = rows[np.argsort(rows[:, 0], kind="stable")]
@@ -143,8 +149,12 @@ def unpack_results(rows: np.ndarray, cells, dataset_name: str, n_evals: int, ela
         from .mcmc import RESULT_FIELDS
 
         results.append({f: r[f] for f in RESULT_FIELDS})
-        t, m, p = cells.cell(c)
-        plots.append({"t_plot": t.copy(), "MS2_plot": m.copy(), "PP7_plot": p.copy(),
+        lc = c - int(cell_offset)
+        if 0 <= lc < cells.n_cells:
+            t, m, p = (a.copy() for a in cells.cell(lc))
+        else:
+            t = m = p = np.zeros(0)
+        plots.append({"t_plot": t, "MS2_plot": m, "PP7_plot": p,
                       "simMS2": row[base + 2 * n_max:base + 2 * n_max + n].copy(),
                       "simPP7": row[base + 3 * n_max:base + 3 * n_max + n].copy()})
         chains.append({})
@@ -152,30 +162,61 @@ def unpack_results(rows: np.ndarray, cells, dataset_name: str, n_evals: int, ela
                      (rows[:, 0].astype(np.int64) - 1))
 
 
-def fit_sharded(lk, group=None, device: Optional[str] = None, v0=None, approved=None, **fit_kwargs):
-    """``TranscriptionCycleMCMC`` over ``torch.distributed`` ranks, one GPU each: rank r fits the
-    contiguous cell range ``shard_bounds`` gives it (its own GPU-resident DRAM chains), then ONE
-    all-gather of the packed per-cell results (RCCL on GPUs, gloo on CPU) gives every rank the
-    whole dataset's ``MCMCresults`` / ``MCMCplot``. The chains' randomness is keyed by cell index
-    (:func:`mcmc.fit`), so the gathered results equal a one-GPU fit of all cells bit for bit.
+def fit_sharded(lk, group=None, device: Optional[str] = None, v0=None, approved=None,
+                cell_offset: Optional[int] = None, **fit_kwargs):
+    """``TranscriptionCycleMCMC`` over ``torch.distributed`` ranks, one GPU each: rank r fits its
+    cells (its own GPU-resident DRAM chains), then ONE all-gather of the packed per-cell results
+    (RCCL on GPUs, gloo on CPU) gives every rank the whole dataset's ``MCMCresults`` / ``MCMCplot``
+    (the parfor's sliced-output assembly, :315-356). The chains' randomness is keyed by the
+    dataset-wide cell index (:func:`mcmc.fit`), so the gathered results equal a one-GPU fit of all
+    cells bit for bit.
+
+    Two layouts:
+    * ``cell_offset=None``: every rank holds the whole dataset in ``lk`` and fits the contiguous
+      range ``shard_bounds`` gives it (balanced by Σ N_c·W̄);
+    * ``cell_offset=k``: ``lk`` holds only this rank's contiguous block of the dataset, starting at
+      dataset-wide index k (each rank loaded its own shard files); every cell of ``lk`` is fitted.
+
     ``v0`` / ``approved``: per-cell inputs over ALL cells (by 1-based cell_index in a mapping, or
-    0-based in a sequence); ``fit`` reads them by cell, so every shard passes them unchanged."""
+    0-based in a sequence); ``fit`` reads them by dataset-wide cell, so every shard passes them
+    unchanged. The result carries the gather's wall time (``gather_s``), the bytes every rank
+    receives in it (``gather_bytes``) and this rank's own ``FitResult`` (``local``: raw chains,
+    final states). Without an initialised process group it is the one-rank case."""
+    import time
+
     import torch
     import torch.distributed as dist
 
     from .mcmc import fit
 
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    on = dist.is_available() and dist.is_initialized()
+    world, rank = (dist.get_world_size(group), dist.get_rank(group)) if on else (1, 0)
     cl = lk.cells
-    b = shard_bounds(cell_weights(cl, lk.construct.L0, v0), world)
-    ids = list(range(int(b[rank]), int(b[rank + 1])))
-    fr = fit(lk, cells=ids, v0=v0, approved=approved, **fit_kwargs) if ids else None
-    n_max = int(np.max(cl.lengths))
-    local = pack_results(fr, n_max) if fr is not None else np.zeros((0, 4 + len(_SCALARS) + 4 * n_max))
-    rows = gather_rows(local, group=group, device=device)
+    if cell_offset is None:
+        b = shard_bounds(cell_weights(cl, lk.construct.L0, v0), world)
+        ids, off = list(range(int(b[rank]), int(b[rank + 1]))), 0
+    else:
+        ids, off = list(range(cl.n_cells)), int(cell_offset)
+    fr = fit(lk, cells=ids, v0=v0, approved=approved, cell_offset=off, **fit_kwargs) if ids else None
+    n_max = int(np.max(cl.lengths)) if cl.n_cells else 0
     dev = torch.device(device) if device else torch.device("cpu")
-    t = torch.tensor([fr.elapsed_ms if fr else 0.0, fr.n_evals if fr else 0], dtype=torch.float64, device=dev)
-    mx = t.clone()
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    return unpack_results(rows, cl, cl.name, int(t[1].item()), float(mx[0].item()))
+    if on and cell_offset is not None:  # shards may differ in their longest cell: one common width
+        t = torch.tensor([n_max], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        n_max = int(t.item())
+    local = pack_results(fr, n_max) if fr is not None else np.zeros((0, 4 + len(_SCALARS) + 4 * n_max))
+    if on:
+        dist.barrier(group)
+    g0 = time.perf_counter()
+    rows = gather_rows(local, group=group, device=device)
+    gather_s = time.perf_counter() - g0
+    ev, ms = (fr.n_evals, fr.elapsed_ms) if fr else (0, 0.0)
+    if on:
+        t = torch.tensor([ms, ev], dtype=torch.float64, device=dev)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        ev, ms = int(t[1].item()), float(mx[0].item())
+    out = unpack_results(rows, cl, cl.name, int(ev), float(ms), cell_offset=off)
+    out.gather_s, out.gather_bytes, out.local = gather_s, int(rows.nbytes), fr
+    return out
