@@ -858,3 +858,22 @@ def test_config4_sharded_fit_is_the_same_at_every_world_size():
     np.testing.assert_array_equal(got, want)
     assert nbytes == want.nbytes and n_evals == one.n_evals
     assert np.median(got[:, 3]) > 0.01  # accept rates
+
+
+def test_adaptint_past_the_adaptation_lds_is_refused_before_any_launch(c_oracle):
+    """ADVICE r04: the adaptation kernel's run table grows with adaptint (8 bytes per window row);
+    an adaptint whose table no longer fits a CU's LDS is refused with TCI_ERANGE up front (nothing
+    launched), and one that fits runs."""
+    from transcriptioncycleinference_amd import Likelihood, _lib
+    from transcriptioncycleinference_amd.mcmc import DramOptions, dram_run
+
+    cells, cs, plan = _restatement_case("config4", c_oracle)[:3]
+    sl = slice(0, 2)
+    with Likelihood(cells, cs, device=0) as L:
+        args = (np.array(plan.cells[:2], np.int32), plan.x0[sl], plan.lower[sl], plan.upper[sl], plan.prior_mu[sl],
+                plan.prior_sig[sl], plan.qcov_diag[sl], 1.0)
+        with pytest.raises(_lib.TciError) as ei:
+            dram_run(L, *args, DramOptions(n_steps=50, burnintime=10, adaptint=20000, stats_from=1))
+        assert ei.value.code == _lib.TCI_ERANGE and "LDS" in str(ei.value)
+        ok = dram_run(L, *args, DramOptions(n_steps=3000, burnintime=10, adaptint=1500, stats_from=1))
+        assert np.all(np.isfinite(ok.mean[:, :207]))

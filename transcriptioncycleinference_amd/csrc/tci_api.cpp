@@ -636,6 +636,15 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
     }
   }
   const int64_t p_max_all = *std::max_element(npar.begin(), npar.end());  // > 208: k_adapt_gt's tile grid
+  // limits of the adaptation window, checked before anything is allocated or launched: the
+  // adaptation kernel's LDS (the window's run table grows with adaptint) and the chain kernels'
+  // 32-bit window-log offsets (adaptint * ld)
+  if (opt->adaptint > 0 && tci::dram_adapt_lds_bytes(p_max_all, opt->adaptint) > 160 * 1024)
+    return fail(ctx, TCI_ERANGE, "tci_dram_run: adaptint " + std::to_string(opt->adaptint) +
+                                     " needs more LDS than a CU has for the adaptation at P = " +
+                                     std::to_string(p_max_all));
+  if ((opt->adaptint > 0 ? opt->adaptint : 100) * ld >= (int64_t)INT32_MAX)
+    return fail(ctx, TCI_ERANGE, "tci_dram_run: adaptint * ld must be < 2^31");
   TCI_HIP(ctx, hipSetDevice(ctx->device));
   DevAllocs A;
   hipError_t e = hipSuccess;
@@ -647,7 +656,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   const int64_t ai = opt->adaptint;
   const int64_t DW = tci::draw_stride(ld);
   const int64_t chunk_cap =
-      std::max<int64_t>(32, (int64_t)(((size_t)TCI_DRAWS_GIB << 30) / (n * (size_t)DW * sizeof(double))));
+      std::max<int64_t>(32, (int64_t)(((size_t)tci::kDrawsGiB << 30) / (n * (size_t)DW * sizeof(double))));
   // Without adaptation the window is 100 rows: the records' merge partition (the same for every engine)
   // and the batched engine's graph block stay small (a 1,000-row window made the batched engine run up
   // to 1,000 steps as plain launches before its first graph replay).
@@ -689,7 +698,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(sigma2, double, n);
   TCI_ALLOC(Rd, double, n * tci::dram_tri_stride(L));
   TCI_ALLOC(cov, double, n * tci::dram_cov_stride(L));
-  TCI_ALLOC(work, double, p_max_all > std::min(208, TCI_ADAPT_GT_FROM) ? n * (size_t)((L + 15) / 16 * 16) * ((L + 15) / 16 * 16) : 1);
+  TCI_ALLOC(work, double, p_max_all > tci::kAdaptGtFrom ? n * (size_t)((L + 15) / 16 * 16) * ((L + 15) / 16 * 16) : 1);
   TCI_ALLOC(cmean, double, n * L);
   TCI_ALLOC(wsum, double, n);
   TCI_ALLOC(window, double, n * (size_t)win * L);

@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "tci_diag.h"
 #include "tci_dram_internal.h"
 #include "tci_eval.h"
 
@@ -798,15 +799,7 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
   }
 }
 
-#ifndef TCI_DRAWS_ABLATE
-#define TCI_DRAWS_ABLATE 0  // diagnostics only (wrong results): bit0 no normals, bit1 no MFMA, bit2 no scalars
-#endif
-#ifndef TCI_DRAWS_WIDE
-#define TCI_DRAWS_WIDE 1  // WALK: 64-row draws passes (k_draws<8, 2, 4, 2>)
-#endif
-#ifndef TCI_DRAWS_WPE
-#define TCI_DRAWS_WPE 4  // waves per SIMD k_draws is compiled for (<= 128 VGPRs)
-#endif
+constexpr int kDrawsWPE = 4;             // waves per SIMD k_draws is compiled for (<= 128 VGPRs)
 constexpr int kDrawsPF = 2;               // R values prefetched this many k-steps ahead (mfma_zr PF)
 constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each), 4-wave workgroups
 enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
@@ -826,18 +819,13 @@ __host__ __device__ inline bool draws_walk_wide(int64_t L) { return draws_lds_by
 // Passes per workgroup: every workgroup reads the chain's R once per pass. FUSED (a few hundred
 // chains): 2 (1: 108.8, 2: 104.7, 4: 123.7 us per TestData chunk); WALK (thousands of chains, P =
 // 207): 4, fewer and longer workgroups reading R fewer times.
-#ifndef TCI_DRAWS_NPASS
-#define TCI_DRAWS_NPASS 1  // fused engine: passes per k_draws workgroup (WALK: 4); 2: 80.4 vs 77.9 us (r04np)
-#endif
-#ifndef TCI_DRAWS_NPASS_WALK
-#define TCI_DRAWS_NPASS_WALK 4
-#endif
-__host__ __device__ inline int draws_passes(bool walk) { return walk ? TCI_DRAWS_NPASS_WALK : TCI_DRAWS_NPASS; }
+// fused engine: 1 pass per k_draws workgroup (2: 80.4 vs 77.9 us per chunk, r04np); WALK: 4
+__host__ __device__ inline int draws_passes(bool walk) { return walk ? 4 : 1; }
 
 // NWD waves per workgroup, CT column tiles per wave and MFMA call (launch_chain_t: 4 and 2); longer
 // rows loop over calls. The wave count and CT only move column tiles between waves and calls: same
 // bits.
-template <int NWD, int CT, int MT = kDrawMT, int WPE = TCI_DRAWS_WPE>
+template <int NWD, int CT, int MT = kDrawMT, int WPE = kDrawsWPE>
 __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE))) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end, int npass) {
   constexpr int kDrawWaves = NWD, kDrawThreads = 64 * NWD;
   constexpr int kDrawCT = CT;
@@ -1079,12 +1067,6 @@ __global__ __launch_bounds__(kThreads) void k_stats(DramState st, DramParams p) 
   window_records(st, p, c, *st.step, lane);
 }
 
-#ifndef TCI_CHAIN_PROFILE
-#define TCI_CHAIN_PROFILE 0  // diagnostics: s_memtime cycles per k_chain phase (wave 0) into st.prof
-#endif
-#ifndef TCI_ADAPT_PROFILE
-#define TCI_ADAPT_PROFILE 0  // diagnostics: s_memtime cycles per k_adapt_mfma phase (thread 0) into st.prof
-#endif
 __device__ __forceinline__ uint64_t stamp() {
 #if TCI_CHAIN_PROFILE || TCI_ADAPT_PROFILE
   uint64_t t;
@@ -1160,7 +1142,9 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   const int P = st.npar[c];
   const int64_t DW = draw_stride(ld);
   // this chain's draws rows (row of step s at (s - s_begin) * DW) and window logs (slot r at r * ld):
-  // 32-bit offsets from per-chain bases (a chunk is <= 1,000 rows), no 64-bit multiplies in the loop
+  // 32-bit offsets from per-chain bases, no 64-bit multiplies in the loop -- tci_dram_run checks that
+  // chunk * draw_stride(ld) and adaptint * ld fit in an int (the draws buffer's 2 GiB cap bounds the
+  // first for every chain count)
   const double* const dchain = st.draws + c * p.chunk * DW;
   double* const wlog = st.window + c * p.win * ld;
   double* const s2lg = st.s2log + c * p.win;
@@ -1745,7 +1729,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
                    int with_records, hipStream_t stream) {
-  const bool wide = p.walk != 0 && TCI_DRAWS_WIDE && draws_walk_wide(st.ld);
+  const bool wide = p.walk != 0 && draws_walk_wide(st.ld);  // WALK: 64-row draws passes (k_draws<8, 2, 4, 2>)
   const size_t lds = (size_t)draws_lds_bytes(st.ld, wide ? kDrawMTWalk : kDrawMT);
   // 4-wave workgroups, 2 column tiles x 2 row tiles per wave and MFMA call (128 VGPRs: four
   // workgroups per CU). Config 4 (WALK, P = 207): 72.7 ms per 1,000 steps with the 8-wave, 2-tile
@@ -1780,9 +1764,6 @@ int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, 
 }
 
 
-#ifndef TCI_ADAPT_ABLATE
-#define TCI_ADAPT_ABLATE 0  // diagnostics only (wrong results): bit0 skip the Cholesky, bit1 skip the covupd passes
-#endif
 
 // This lane's index computed afresh (v_mbcnt). The adaptation kernels run at their register budget,
 // where the compiler keeps lane-derived indices alive across whole phases and spills them: a scratch
@@ -1921,30 +1902,37 @@ __device__ __forceinline__ void chol16_finish(double (&a)[4], double* dpiv, doub
 // scatter runs once per run, weighted by its length -- about 1 + 100 x the acceptance rate of the
 // 100 rows; the same sum in exact arithmetic, rounded differently from row-by-row sums (and the
 // same in every engine). Wave w of NW compares rows w, w + NW, .. with their predecessors (any
-// entry unequal, NaN included: a new run), RU rows' loads in flight together; wave 0 then lists
-// the run starts in row order. rs[0..m) = start rows, rs[m] = nb; rf: nb ints of LDS scratch.
+// entry unequal, NaN included: a new run), RU rows' loads in flight together, over every column
+// (blocks of 64 NJA; one block while P <= 64 NJA); wave 0 then lists the run starts in row order.
+// rs[0..m) = start rows, rs[m] = nb; rf: nb ints of LDS scratch.
 template <int NW, int NJA, int RU>
 __device__ int window_runs(const double* win, int64_t ld, int P, int nb, int* rs, int* rf, int* nrun) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   for (int r0 = w; r0 < nb; r0 += RU * NW) {  // uniform per wave
-    double a[RU][NJA], b[RU][NJA];
+    bool d[RU];
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int r = min(r0 + u * NW, nb - 1), rp = max(r - 1, 0);
+    for (int u = 0; u < RU; ++u) d[u] = r0 + u * NW == 0;
+    for (int j0 = 0; j0 < P; j0 += 64 * NJA) {  // uniform
+      double a[RU][NJA], b[RU][NJA];
 #pragma unroll
-      for (int k = 0; k < NJA; ++k) {
-        const int j = min(lane + 64 * k, P - 1);
-        a[u][k] = win[(int64_t)r * ld + j];
-        b[u][k] = win[(int64_t)rp * ld + j];
+      for (int u = 0; u < RU; ++u) {
+        const int r = min(r0 + u * NW, nb - 1), rp = max(r - 1, 0);
+#pragma unroll
+        for (int k = 0; k < NJA; ++k) {
+          const int j = min(j0 + lane + 64 * k, P - 1);
+          a[u][k] = win[(int64_t)r * ld + j];
+          b[u][k] = win[(int64_t)rp * ld + j];
+        }
       }
+#pragma unroll
+      for (int u = 0; u < RU; ++u)
+#pragma unroll
+        for (int k = 0; k < NJA; ++k) d[u] = d[u] || !(a[u][k] == b[u][k]);
     }
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int r = r0 + u * NW;
-      bool d = r == 0;
-#pragma unroll
-      for (int k = 0; k < NJA; ++k) d = d || !(a[u][k] == b[u][k]);
-      const bool any = wave_ballot(d) != 0;
+      const bool any = wave_ballot(d[u]) != 0;
       if (lane == 0 && r < nb) rf[r] = any ? 1 : 0;
     }
   }
@@ -1967,10 +1955,7 @@ __device__ int window_runs(const double* win, int64_t ld, int P, int nb, int* rs
   return *nrun;
 }
 
-#ifndef TCI_AD_RB
-#define TCI_AD_RB 16
-#endif
-constexpr int kAdRB = TCI_AD_RB;  // window runs per LDS batch
+constexpr int kAdRB = 16;  // window runs per LDS batch
 __host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P, int64_t nb) {
   const int64_t NT = (P + 15) / 16, LX = 16 * NT;
   const int64_t shared = 2 * kAdRB * LX > 2 * NT * 256 ? 2 * kAdRB * LX : 2 * NT * 256;  // X, Xw | panel buffers
@@ -2342,7 +2327,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
   const double na = st.wsum[c], nn = na + (double)p.adaptint;
   const double fcross = na * (double)p.adaptint / nn;
   const double rn1 = 1.0 / (nn - 1.0);
-  const int M = window_runs<NW, 9, 1>(win, ld, P, nb, rs, rf, &nrun);  // P <= 576
+  const int M = window_runs<NW, 9, 1>(win, ld, P, nb, rs, rf, &nrun);  // any P (blocks of 576 columns)
   // ---- covupd: scatter of the centred window runs (each row once, times its run length) + merge,
   //      kGtTiles tiles per wave and pass
   for (int base = 0; base < T; base += NW * kGtTiles) {
@@ -2633,7 +2618,7 @@ int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
   // TestData adaptation against 4 waves x 12 tiles (r03af; 28 VGPRs spilled, still faster)
   if (p.pmax <= 16 * 9) return launch_adapt_mfma<8, 9, 6, 4>(st, p, stream);
   // P <= 208: 8 waves x 12 tiles (16 waves x 6 tiles measured slower)
-  if (p.pmax <= 16 * 13 && p.pmax <= TCI_ADAPT_GT_FROM) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
+  if (p.pmax <= 16 * 13 && p.pmax <= kAdaptGtFrom) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
   const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax, p.adaptint);
   if (ensure_dyn_lds((const void*)k_adapt_gt, lds) != TCI_OK) return TCI_EHIP;
   hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.n_chains), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);
@@ -2649,6 +2634,11 @@ int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& k
     case 8: return launch_chain_r<8>(st, p, kp, s_begin, s_end, with_records, s);
     default: return TCI_EINVAL;
   }
+}
+int64_t dram_adapt_lds_bytes(int64_t pmax, int64_t adaptint) {
+  if (adaptint <= 0) return 0;
+  if (pmax <= 16 * 9 || (pmax <= 16 * 13 && pmax <= kAdaptGtFrom)) return adapt_mfma_lds_bytes(pmax, adaptint);
+  return adapt_gt_lds_bytes(pmax, adaptint);
 }
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl) {
   const int64_t ns = 4 * (rpl <= 2 ? kChainEPW : 1);  // k_chain: evl, yl, xch, xip (and slack)

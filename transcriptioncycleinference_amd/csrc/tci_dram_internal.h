@@ -19,12 +19,12 @@ constexpr int64_t dram_cov_stride(int64_t ld) {
   return ld * ld > (ld + 15) / 16 * ((ld + 15) / 16 + 1) / 2 * 256 ? ld * ld : (ld + 15) / 16 * ((ld + 15) / 16 + 1) / 2 * 256;
 }
 
-#ifndef TCI_DRAWS_GIB
-#define TCI_DRAWS_GIB 2  // the fused engine's draws buffer: at most this many GiB (sets the chunk length)
-#endif
-#ifndef TCI_ADAPT_GT_FROM
-#define TCI_ADAPT_GT_FROM 208  // rows longer than this adapt with k_adapt_gt (tiles in global memory)
-#endif
+// The fused engine's draws buffer: at most this many GiB (sets the chunk length; an 8 GiB buffer
+// measured within noise, r04s).
+constexpr int64_t kDrawsGiB = 2;
+// Rows longer than this adapt with k_adapt_gt (tiles in global memory); k_adapt_mfma<8, 13, 12> up to
+// here (k_adapt_gt at config 4's P = 207: 5,207 -> 5,887 us, r04q).
+constexpr int64_t kAdaptGtFrom = 208;
 
 struct DramState {
   int64_t n_chains;
@@ -116,6 +116,10 @@ int dram_launch_init_stats(const DramState& st, const DramParams& p, void* strea
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,
                       int64_t s_end, int with_records, void* stream);
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl);  // LDS per workgroup of the fused engine
+// Dynamic LDS of the adaptation kernel dram_launch_adapt picks for (pmax, adaptint): the window's run
+// table grows with adaptint (8 bytes per row), so tci_dram_run refuses an adaptint past the CU's LDS
+// before any launch.
+int64_t dram_adapt_lds_bytes(int64_t pmax, int64_t adaptint);
 // The records of the window of chain rows ending at row *st.step (posterior mean / M2, window column
 // sums, s2 statistics, thinned outputs) from the rows every engine logs: run after a window's last
 // row (a multiple of p.win) and after the chain's last row (the batched engine; the fused engines

@@ -49,12 +49,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include "tci_diag.h"
 #include "tci_internal.h"
-
-// Build-time variants for A/B timing (scripts/ab_variants.py); the shipped defaults are below.
-#ifndef TCI_ABLATE
-#define TCI_ABLATE 0         // diagnostics only (wrong results): bit0 rows, bit2 interp, bit3 scan, bit4 loads only, bit5 launch only
-#endif
 
 namespace tci {
 
@@ -162,16 +158,6 @@ __device__ __forceinline__ double max_f64(double a, double b) {
   asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
-// the same with a wave-uniform b as an SGPR-pair operand (no copy of b into VGPRs)
-__device__ __forceinline__ double max_f64s(double a, double b) {
-  double r;
-  const double bs = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(b)),
-                                     __builtin_amdgcn_readfirstlane(__double2loint(b)));
-  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "s"(bs));
-  return r;
-}
-template <bool SB>
-__device__ __forceinline__ double max_basal(double a, double b) { return SB ? max_f64s(a, b) : max_f64(a, b); }
 
 // Exponent field of a double: all ones iff the value is +-Inf or NaN. The max over the
 // wave-uniform theta entries stays on the scalar unit (isfinite() would be a vector compare each).
@@ -332,7 +318,7 @@ __device__ __forceinline__ void load_cell(const KParams& kp, int c, int lane, Ev
 // 2 <= N = e.cm.n <= 64*RPL + 1. aux (MODE_SS, optional): a per-lane partial on entry, its wave sum
 // (lane63(wave_incl_scan), the same bits) on return -- reduced together with the SS (the DRAM chain
 // kernel's prior).
-template <int RPL, int NSEG, int MODE, bool SB = false>  // SB: b1/b2 wave-uniform in SGPRs (max_f64s)
+template <int RPL, int NSEG, int MODE>
 __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>& e, int lane, double* lds,
                                             int64_t b, double* __restrict__ out0, double* __restrict__ out1,
                                             int64_t ld_out, double* aux = nullptr) {
@@ -565,11 +551,11 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
 #pragma unroll
   for (int q = 0; q < RPL; ++q) {
     // MS2(MS2 < basal) = basal == max(MS2, basal): the sums are finite and >= 0 here
-    double m = max_basal<SB>(accM[0][q], b1), pp = max_basal<SB>(accP[0][q], b2);
+    double m = max_f64(accM[0][q], b1), pp = max_f64(accP[0][q], b2);
 #pragma unroll
     for (int k = 1; k < NSEG; ++k) {
-      m = max_basal<SB>(m + accM[k][q], b1);
-      pp = max_basal<SB>(pp + accP[k][q], b2);
+      m = max_f64(m + accM[k][q], b1);
+      pp = max_f64(pp + accP[k][q], b2);
     }
     rowM[q] = A * m;
     rowP[q] = pp;

@@ -9,27 +9,17 @@ namespace {
 // 4 independent waves per 256-thread block (1- and 8-wave blocks measured no faster). Round 2: a
 // register budget for 6 waves/SIMD took 50 vs 58 us per launch at the compiler's default 5, and 7-8
 // were no faster then; with round 3's shorter instruction stream 8 pays (below).
-// (An XCD-aware block -> row-range order measured ~1 % slower: the cell table fits every XCD's L2.)
-#ifndef TCI_LK_WPB
-#define TCI_LK_WPB 4
-#endif
-#ifndef TCI_LK_XCD
-#define TCI_LK_XCD 0  // 1: block -> row range by XCD (round-robin dispatch: block i runs on XCD i % 8)
-#endif
-#ifndef TCI_LK_SB
-#define TCI_LK_SB 0   // 1: the basal floors take theta's b1/b2 as SGPR operands
-#endif
-constexpr int kWavesPerBlock = TCI_LK_WPB;
+// (An XCD-aware block -> row-range order and SGPR basal operands measured within noise: DESIGN.md
+// Appendix A.)
+constexpr int kWavesPerBlock = 4;
 // Waves per SIMD the register budget is set for: 8 while RPL * NSEG <= 2 (58 VGPRs at RPL = 2,
 // NSEG = 1, no spill; 34.4 vs 36.0 us per bench launch against 6 in one process,
 // profiles/r03_likelihood/r03occ1_ab.json; 7: 35.8), 6 above (RPL = 2 with two segments spills at
 // 8; the LDS of a 4-wave block caps RPL = 4 at 4 waves/SIMD anyway).
-#ifndef TCI_LK_WPE
-#define TCI_LK_WPE(RPL, NSEG) ((RPL) * (NSEG) <= 2 ? 8 : 6)
-#endif
+constexpr int lk_waves_per_eu(int rpl, int nseg) { return rpl * nseg <= 2 ? 8 : 6; }
 
 template <int RPL, int NSEG, int MODE>
-__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(TCI_LK_WPE(RPL, NSEG)))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
+__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(lk_waves_per_eu(RPL, NSEG)))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
@@ -39,14 +29,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int64_t blk = blockIdx.x;
-  if (TCI_LK_XCD) {
-    // the 8 XCDs take blocks round-robin (block i on XCD i % 8): XCD x gets the contiguous block
-    // range [x q, x q + q) of the first 8 q blocks, so its L2 holds only its rows' cells
-    const int64_t G = gridDim.x, q = G >> 3;
-    if (blk < 8 * q) blk = (blk & 7) * q + (blk >> 3);
-  }
-  const int64_t b = blk * kWavesPerBlock + wid;
+  const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wid;
   if (b >= B) return;
   double* lds = s_lds[wid];
 #if TCI_ABLATE & 32
@@ -108,7 +91,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
     write_nan<MODE>(lane, N, b, out0, out1, ld_out);
     return;
   }
-  const double ss = eval_wave<RPL, NSEG, MODE, TCI_LK_SB != 0>(kp, e, lane, lds, b, out0, out1, ld_out);
+  const double ss = eval_wave<RPL, NSEG, MODE>(kp, e, lane, lds, b, out0, out1, ld_out);
   if (MODE == MODE_SS && lane == 0) out0[b] = ss;
 }
 
