@@ -11,7 +11,8 @@ i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
            "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT" \
-           "TA_BUSY_avr TA_BUSY_max GRBM_GUI_ACTIVE"; do
+           "TA_BUSY_avr TA_BUSY_max GRBM_GUI_ACTIVE" \
+           "TCC_HIT_sum TCC_MISS_sum SQ_INSTS_SMEM SQ_INSTS_FLAT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   echo "== pass $i: $grp"
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/${TAG}_p$i" -o pmc -- \

@@ -18,7 +18,7 @@ import sys
 
 def main(prefix, workload):
     agg = collections.defaultdict(list)
-    for p in range(1, 7):
+    for p in range(1, 8):
         files = glob.glob(f"{prefix}_p{p}/**/*counter_collection.csv", recursive=True)
         rows = [r for f in files for r in csv.DictReader(open(f))]
         for r in rows:

@@ -409,6 +409,37 @@ def test_device_async_api_matches_host_api(lk, chain):
     np.testing.assert_array_equal(out_d.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("offset", [0, 1, 2, 3])
+@pytest.mark.parametrize("B", [4093, 4096, 4097, 5])
+def test_active_flags_at_every_alignment_and_length(lk, chain, offset, B):
+    """The kernel reads the active flags by 4-byte words through the scalar cache where the word lies
+    inside the flag array (and the array is 4-byte aligned), byte by byte elsewhere: flag arrays at
+    every byte offset of an allocation and batch lengths on and off a multiple of 4 give the host
+    API's results row for row (+Inf for every inactive row)."""
+    import torch
+
+    rows = pack(chain["rows"])
+    rng = np.random.default_rng(B + offset)
+    idx = rng.integers(0, len(rows), B)
+    theta, cid = rows[idx], chain["cell_id"][idx].astype(np.int32)
+    act = (rng.random(B) < 0.7).astype(np.uint8)
+    act[-1] = 1
+    act[-2:] = [0, 1] if B > 2 else act[-2:]
+    want = lk.ss_batch(theta, cid, act)
+    dev = torch.device("cuda:0")
+    base = torch.zeros(B + 8, dtype=torch.uint8, device=dev)
+    act_d = base[offset:offset + B]
+    act_d.copy_(torch.from_numpy(act))
+    th_d = torch.from_numpy(theta).to(dev)
+    cid_d = torch.from_numpy(cid).to(dev)
+    out_d = torch.empty(B, dtype=torch.float64, device=dev)
+    lk.ss_batch_device(th_d, cid_d, out_d, act_d, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    got = out_d.cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+    assert np.all(np.isinf(got[act == 0])) and np.all(np.isfinite(got[act == 1]))
+
+
 # --- reference-named API -------------------------------------------------------------
 
 

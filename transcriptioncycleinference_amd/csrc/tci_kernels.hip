@@ -6,12 +6,17 @@ namespace tci {
 
 namespace {
 
-// 4 independent waves per 256-thread block (1- and 8-wave blocks measured no faster). Round 2: a
-// register budget for 6 waves/SIMD took 50 vs 58 us per launch at the compiler's default 5, and 7-8
-// were no faster then; with round 3's shorter instruction stream 8 pays (below).
-// (An XCD-aware block -> row-range order and SGPR basal operands measured within noise: DESIGN.md
-// Appendix A.)
-constexpr int kWavesPerBlock = 4;
+// One wave per 64-thread block (round 5): a block's LDS is held until its last wave ends, so with
+// 4-wave blocks every bounds-rejected row (a wave that exits at once) kept its 4 KB of LDS allocated
+// beside its block's evaluating waves and LDS, not the wave slots, capped the evaluating waves per CU
+// (~28 % of the bench's rows are rejected). 1-wave blocks: 33.6 vs 35.4 us per bench launch; with the
+// flag read through the scalar cache (below) 32.9 (profiles/r05/r05h_lk.json). Round 2: a register
+// budget for 6 waves/SIMD took 50 vs 58 us per launch at the compiler's default 5, and 7-8 were no
+// faster then; with round 3's shorter instruction stream 8 pays (below). (An XCD-aware block -> row
+// order, SGPR basal operands, cell records shared through LDS by a 4-wave block (45.6 vs 35.2) and
+// every load of the evaluation issued with the flag's (40.7 vs 35.2) measured slower or within noise:
+// DESIGN.md Appendix A.)
+constexpr int kWavesPerBlock = 1;
 // Waves per SIMD the register budget is set for: 8 while RPL * NSEG <= 2 (58 VGPRs at RPL = 2,
 // NSEG = 1, no spill; 34.4 vs 36.0 us per bench launch against 6 in one process,
 // profiles/r03_likelihood/r03occ1_ab.json; 7: 35.8), 6 above (RPL = 2 with two segments spills at
@@ -23,7 +28,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
-                                                         int64_t ld_out) {
+                                                         int64_t ld_out, int64_t flag_words) {
   constexpr int WAVE_DOUBLES = eval_lds_doubles<RPL>();  // {K,J} table / the two sim rows
   __shared__ __attribute__((aligned(16))) double s_lds[kWavesPerBlock][WAVE_DOUBLES];
 
@@ -41,7 +46,14 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
   //      reading the theta scalars with the cell id, one round trip earlier, measured no faster and
   //      fetched the theta lines of the bounds-rejected rows too: DESIGN.md §3.)
   const int c = __builtin_amdgcn_readfirstlane(cell_id[b]);
-  const bool act = MODE != MODE_SS || active == nullptr || active[b] != 0;
+  // the flag through the scalar cache (one s_load_dword of its 4-byte word): a rejected row's wave
+  // ends without queueing behind the other waves' vector loads (34.2 vs 35.4 us per bench launch,
+  // r05h). flag_words: the rows whose whole word lies inside `active` (which is 4-byte aligned);
+  // the last partial word and a misaligned array read the byte.
+  bool act = true;
+  if (MODE == MODE_SS && active != nullptr)
+    act = b < flag_words ? ((reinterpret_cast<const uint32_t*>(active)[b >> 2] >> (8 * (b & 3))) & 0xffu) != 0
+                         : active[b] != 0;
   if (!act) {
     if (lane == 0) out0[b] = INFINITY;  // skipped proposal (bounds-rejected by the caller)
     return;
@@ -100,8 +112,9 @@ void launch_one(const KParams& kp, const double* theta, int64_t ld, const int32_
                 int64_t B, double* out0, double* out1, int64_t ld_out, hipStream_t stream) {
   const dim3 block(64 * kWavesPerBlock);
   const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock));
+  const int64_t flag_words = active != nullptr && (reinterpret_cast<uintptr_t>(active) & 3) == 0 ? (B & ~(int64_t)3) : 0;
   hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE>), grid, block, 0, stream, kp, theta, ld, cell_id, active, B,
-                     out0, out1, ld_out);
+                     out0, out1, ld_out, flag_words);
 }
 
 template <int RPL, int NSEG>
