@@ -1509,12 +1509,16 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 // one-workgroup-per-chain layout does. Every value is computed by the same expressions as
 // k_chain (its step-s lanes) and the batched engine: identical chains (tests/test_dram_gpu.py).
 // Register budget: two waves per SIMD (229 -> 188 us per config-4 step).
+#ifndef TCI_WALK_WPB
+#define TCI_WALK_WPB 4  // experiment (round 5): chains (waves) per k_walk workgroup
+#endif
+constexpr int kWalkWaves = TCI_WALK_WPB;
 template <int RPL, int NSEG>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_walk(DramState st, DramParams p, KParams kp, int64_t s_begin,
+__global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu(2))) void k_walk(DramState st, DramParams p, KParams kp, int64_t s_begin,
                                                                 int64_t s_end, int with_records) {
   constexpr int NJ = RPL + 1;
   constexpr int EV = eval_lds_doubles<RPL>();
-  constexpr int NW = kThreads / 64;
+  constexpr int NW = kWalkWaves;
   __shared__ __attribute__((aligned(16))) double evl[NW][EV];  // each wave's {K,J} tables / rows
   __shared__ double yl[NW][64 * NJ];                            // each wave's proposal (theta broadcast)
   __shared__ double racc[NW][3][64 * NJ];  // each wave's window column sums ws, S1, S2 (ColAcc, in LDS)
@@ -1743,7 +1747,8 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
   hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(64 * nwd), lds, stream, st, p, s_begin, s_end, npass);
   if (p.walk)
-    hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + 3) / 4)), dim3(kThreads), 0, stream, st, p,
+    hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + kWalkWaves - 1) / kWalkWaves)),
+                       dim3(64 * kWalkWaves), 0, stream, st, p,
                        kp, s_begin, s_end, with_records);
   else
     hipLaunchKernelGGL((k_chain<RPL, NSEG, (RPL <= 2 ? kChainEPW : 1)>), dim3((unsigned)st.n_chains), dim3(kThreads), 0,
