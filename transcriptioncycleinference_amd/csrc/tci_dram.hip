@@ -1505,14 +1505,13 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
 
 // One wavefront per chain (the WALK engine: many chains, e.g. configs 4/5's 10,000): the same
 // chunk of rows as k_chain, step by step, stage 2 evaluated only when stage 1 is rejected. No
-// workgroup barriers; 4 chains per 256-thread workgroup, so a CU holds 4x the chains k_chain's
-// one-workgroup-per-chain layout does. Every value is computed by the same expressions as
+// workgroup barriers; one chain per 64-thread workgroup (a CU holds 8 of them at the register
+// budget, 2x the chains k_chain's 4-wave layout does). Every value is computed by the same expressions as
 // k_chain (its step-s lanes) and the batched engine: identical chains (tests/test_dram_gpu.py).
 // Register budget: two waves per SIMD (229 -> 188 us per config-4 step).
-#ifndef TCI_WALK_WPB
-#define TCI_WALK_WPB 4  // experiment (round 5): chains (waves) per k_walk workgroup
-#endif
-constexpr int kWalkWaves = TCI_WALK_WPB;
+// One chain (wave) per workgroup: a 4-chain workgroup kept its 74 KB of LDS until its slowest chain
+// ended (config 4: k_walk 2,189 -> 2,135 us per chunk, bitwise equal, profiles/r05/r05ic4_*).
+constexpr int kWalkWaves = 1;
 template <int RPL, int NSEG>
 __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu(2))) void k_walk(DramState st, DramParams p, KParams kp, int64_t s_begin,
                                                                 int64_t s_end, int with_records) {

@@ -6,7 +6,7 @@ namespace tci {
 
 namespace {
 
-// One wave per 64-thread block (round 5): a block's LDS is held until its last wave ends, so with
+// One wave per 64-thread block for RPL <= 2 (round 5): a block's LDS is held until its last wave ends, so with
 // 4-wave blocks every bounds-rejected row (a wave that exits at once) kept its 4 KB of LDS allocated
 // beside its block's evaluating waves and LDS, not the wave slots, capped the evaluating waves per CU
 // (~28 % of the bench's rows are rejected). 1-wave blocks: 33.6 vs 35.4 us per bench launch; with the
@@ -15,8 +15,12 @@ namespace {
 // faster then; with round 3's shorter instruction stream 8 pays (below). (An XCD-aware block -> row
 // order, SGPR basal operands, cell records shared through LDS by a 4-wave block (45.6 vs 35.2) and
 // every load of the evaluation issued with the flag's (40.7 vs 35.2) measured slower or within noise:
-// DESIGN.md Appendix A.)
-constexpr int kWavesPerBlock = 1;
+// DESIGN.md Appendix A.) RPL >= 4 (cells of 130-513 points) keeps 4-wave blocks: there the 1-wave
+// layout let the compiler take 127 instead of 98 VGPRs at the same occupancy and the config-4 kernel
+// slowed from 107 to 123 us per launch (profiles/r05/r05i_bench.json).
+template <int RPL>
+constexpr int waves_per_block() { return RPL <= 2 ? 1 : 4; }
+
 // Waves per SIMD the register budget is set for: 8 while RPL * NSEG <= 2 (58 VGPRs at RPL = 2,
 // NSEG = 1, no spill; 34.4 vs 36.0 us per bench launch against 6 in one process,
 // profiles/r03_likelihood/r03occ1_ab.json; 7: 35.8), 6 above (RPL = 2 with two segments spills at
@@ -24,12 +28,13 @@ constexpr int kWavesPerBlock = 1;
 constexpr int lk_waves_per_eu(int rpl, int nseg) { return rpl * nseg <= 2 ? 8 : 6; }
 
 template <int RPL, int NSEG, int MODE>
-__global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_per_eu(lk_waves_per_eu(RPL, NSEG)))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
+__global__ __launch_bounds__(64 * waves_per_block<RPL>()) __attribute__((amdgpu_waves_per_eu(lk_waves_per_eu(RPL, NSEG)))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
                                                          int64_t ld_out, int64_t flag_words) {
   constexpr int WAVE_DOUBLES = eval_lds_doubles<RPL>();  // {K,J} table / the two sim rows
+  constexpr int kWavesPerBlock = waves_per_block<RPL>();
   __shared__ __attribute__((aligned(16))) double s_lds[kWavesPerBlock][WAVE_DOUBLES];
 
   const int lane = threadIdx.x & 63;
@@ -110,6 +115,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) __attribute__((amdgpu_waves_pe
 template <int RPL, int NSEG, int MODE>
 void launch_one(const KParams& kp, const double* theta, int64_t ld, const int32_t* cell_id, const uint8_t* active,
                 int64_t B, double* out0, double* out1, int64_t ld_out, hipStream_t stream) {
+  constexpr int kWavesPerBlock = waves_per_block<RPL>();
   const dim3 block(64 * kWavesPerBlock);
   const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock));
   const int64_t flag_words = active != nullptr && (reinterpret_cast<uintptr_t>(active) & 3) == 0 ? (B & ~(int64_t)3) : 0;
