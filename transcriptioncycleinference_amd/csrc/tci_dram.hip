@@ -1809,77 +1809,105 @@ __device__ __forceinline__ double row_to_all(double x) {
   return __hiloint2double((int)h[1], (int)h[0]);
 }
 
-// Steps K and K+1 (K even) of the Cholesky factorization A = U'U of a symmetric 16 x 16 tile held
-// by ONE wave in registers, in the MFMA accumulator layout (lane 16 g + j holds rows g, g+4, g+8,
-// g+12 of column j). Pivot by pivot, rows and columns > K take the symmetric rank-1 update
-// A -= a_K a_K' / d (both triangles, so column K is a row broadcast); row K keeps A[K][j] and its
-// pivot d goes to dpiv[K]; the square roots are left to chol16_finish. Two pivots per call: the
-// pivot-block entries are read together and every element takes both rank-1 updates back to back,
-// with the operands the one-pivot recurrence forms -- the column-(K+1) values after step K,
-// A'[i][K+1] = fma(-A[i][K], A[K][K+1]*rd0, A[i][K+1]), row K+1 after step K,
-// A'[K+1][j] = fma(-A[K+1][K], A[K][j]*rd0, A[K+1][j]), and the pivot d1' from it -- so the bits
-// are the one-pivot form's (bitwise-equal fits, r03ag). Half the pivot round trips (readlane ->
-// v_rcp_f64 + Newton -> update -> readlane) of the one wave that factors the tile, ~25 % fewer
-// instructions: k_adapt_mfma 112.2 -> 109.3 us per TestData adaptation (r03af).
-template <int K, bool F = false>
-__device__ __forceinline__ void chol16_step2(double (&a)[4], double* dpiv, bool& bad) {
-  if constexpr (K < 16) {
-    constexpr int kg0 = K & 3, kr0 = K >> 2, kg1 = (K + 1) & 3, kr1 = (K + 1) >> 2;
-    const int lane = lane_idx<F>(), g = lane >> 4, j = lane & 15;
-    const double d0 = lane_bcast(a[kr0], 16 * kg0 + K);      // A[K][K]
-    const double b = lane_bcast(a[kr0], 16 * kg0 + K + 1);   // A[K][K+1]
-    const double bl = lane_bcast(a[kr1], 16 * kg1 + K);      // A[K+1][K] (the updates leave the two
-                                                              // triangles equal only up to rounding)
-    const double d1 = lane_bcast(a[kr1], 16 * kg1 + K + 1);  // A[K+1][K+1]
-    const double akj0 = row_to_all<kg0>(a[kr0]);              // A[K][j]
-    const double akj1 = row_to_all<kg1>(a[kr1]);              // A[K+1][j]
-    double aik0[4], aik1[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      aik0[q] = row_bcast16<K>(a[q]);      // A[g + 4q][K]
-      aik1[q] = row_bcast16<K + 1>(a[q]);  // A[g + 4q][K+1]
-    }
-    double rd0 = __builtin_amdgcn_rcp(d0);
-    rd0 = fma(rd0, fma(-d0, rd0, 1.0), rd0);
-    const double sj0 = akj0 * rd0;
-    const double s01 = b * rd0;                    // sj0 of column K+1
-    const double d1p = fma(-bl, s01, d1);          // A'[K+1][K+1]
-    double rd1 = __builtin_amdgcn_rcp(d1p);
-    rd1 = fma(rd1, fma(-d1p, rd1, 1.0), rd1);
-    const double akj1p = j > K ? fma(-bl, sj0, akj1) : akj1;  // A'[K+1][j] (row K+1 after step K)
-    const double sj1 = akj1p * rd1;
-    bad = bad || !(d0 > 0.0) || !isfinite(d0) || !(d1p > 0.0) || !isfinite(d1p);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = g + 4 * q;
-      const double aik1p = fma(-aik0[q], s01, aik1[q]);  // A'[i][K+1]
-      double t = a[q];
-      if (i > K && j > K) t = fma(-aik0[q], sj0, t);
-      if (i > K + 1 && j > K + 1) t = fma(-aik1p, sj1, t);
-      a[q] = t;
-    }
-    if (lane == 0) {
-      dpiv[K] = d0;
-      dpiv[K + 1] = d1p;
-    }
-    chol16_step2<K + 2, F>(a, dpiv, bad);
+// Cholesky factorization A = U'U of a symmetric 16 x 16 tile held by ONE wave in registers, in the
+// MFMA accumulator layout (lane 16 g + j holds rows g, g+4, g+8, g+12 of column j: slot q = rows
+// 4q .. 4q+3), blocked by 4 pivots. Block B is slot B: its four pivots K = 4B + r eliminate inside the
+// slot only (rows 4B + g > K of columns j > K take A -= A[.][K] A[K][j] / d, column K a DPP row
+// broadcast, row K a permlane row broadcast), the slot's rows are scaled to U rows (1 / sqrt(d) per
+// row), and the trailing rows and columns >= 4B + 4 take the rank-4 update A -= U_B' U_B as ONE
+// v_mfma_f64_16x16x4 -- the slot itself is both operands (A[i][k] = U[4B+k][i] sits in lane 16 k + i,
+// the B operand's lane for U[4B+k][j]), zeroed in the columns < 4B + 4. The pivot round trip
+// (readlane -> reciprocal -> update) stays on one slot instead of four and 12 of the 15 rank-1
+// updates of the whole tile become 3 MFMAs. rdg[4B + g] = 1 / U[4B+g][4B+g] for the panel solve;
+// bad if a pivot is not positive and finite.
+template <int B, int R, bool F>
+__device__ __forceinline__ void chol16_pivot(double& x, double& dv, bool& bad) {
+  constexpr int K = 4 * B + R;
+  const int lane = lane_idx<F>(), g = lane >> 4, j = lane & 15;
+  const double d = lane_bcast(x, 16 * R + K);  // A[K][K]
+  bad = bad || !(d > 0.0) || !isfinite(d);
+  if (g == R) dv = d;
+  if constexpr (R < 3) {
+    const double akj = row_to_all<R>(x);   // A[K][j]
+    const double aik = row_bcast16<K>(x);  // A[4B + g][K]
+    double rd = __builtin_amdgcn_rcp(d);
+    rd = fma(rd, fma(-d, rd, 1.0), rd);
+    const double sj = akj * rd;
+    if (g > R && j > K) x = fma(-aik, sj, x);
   }
 }
 
-// After the 16 steps: U[i][j] = A[i][j] / sqrt(d_i) for j >= i; rdg[i] = 1 / U[i][i] for the panel
-// solve (dpiv and rdg may alias: each lane reads its pivots before the diagonal lanes write).
-template <bool F = false>
-__device__ __forceinline__ void chol16_finish(double (&a)[4], double* dpiv, double* rdg) {
-  const int lane = lane_idx<F>(), g = lane >> 4, j = lane & 15;
-  double rs[4];
+template <int B, bool F>
+__device__ __forceinline__ void chol16_block(double (&a)[4], double* rdg, bool& bad) {
+  if constexpr (B < 4) {
+    const int lane = lane_idx<F>(), g = lane >> 4, j = lane & 15;
+    double x = a[B], dv = 1.0;
+    chol16_pivot<B, 0, F>(x, dv, bad);
+    chol16_pivot<B, 1, F>(x, dv, bad);
+    chol16_pivot<B, 2, F>(x, dv, bad);
+    chol16_pivot<B, 3, F>(x, dv, bad);
+    const double rs = 1.0 / sqrt(dv);
+    const double u = x * rs;  // U[4B + g][j] for j >= 4B + g
+    if (j == 4 * B + g) rdg[j] = rs;
+    if constexpr (B < 3) {
+      const double op = j >= 4 * B + 4 ? u : 0.0;
+      f64x4 acc = {a[0], a[1], a[2], a[3]};
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-op, op, acc, 0, 0, 0);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) rs[q] = 1.0 / sqrt(dpiv[g + 4 * q]);
-  wave_sync();
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    a[q] = a[q] * rs[q];
-    if (j == g + 4 * q) rdg[j] = rs[q];
+      for (int q = 0; q < 4; ++q) a[q] = acc[q];
+    }
+    a[B] = u;
+    chol16_block<B + 1, F>(a, rdg, bad);
   }
+}
+
+template <bool F = false>
+__device__ __forceinline__ void chol16(double (&a)[4], double* rdg, bool& bad) {
+  chol16_block<0, F>(a, rdg, bad);
+}
+
+// The panel solve U' X = A of one 16 x 16 row tile, held by one wave in the MFMA layout (x[q]: rows
+// g + 4q of column j), U the panel's diagonal tile row-major in LDS (D[k 16 + m] = U[k][m], m >= k)
+// and rdg[k] = 1 / U[k][k]. Blocked like chol16: the four rows of slot B are solved in turn (row r
+// scaled by rdg, broadcast to the slot's later rows by permlanes, fma with U[4B+r][4B+g]), then the
+// rows below take X -= U_B' X_B as one MFMA (A operand: U[4B+k][i] for i >= 4B + 4, B operand: the
+// slot). Every coefficient is an LDS load independent of the recurrence (the 16-lane column loop
+// waited on 136 dependent-order LDS reads).
+template <int B, bool F>
+__device__ __forceinline__ void solve16_block(double (&x)[4], const double* D, const double* rdg) {
+  if constexpr (B < 4) {
+    const int lane = lane_idx<F>(), g = lane >> 4, j = lane & 15;
+    const double rg = rdg[4 * B + g];
+    double cf[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) cf[r] = D[(4 * B + r) * 16 + 4 * B + g];  // U[4B+r][4B+g], used for g > r
+    const double aop = (B < 3 && j >= 4 * B + 4) ? D[(4 * B + g) * 16 + j] : 0.0;
+    double xb = x[B];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (g == r) xb = xb * rg;
+      if (r < 3) {
+        double t;
+        if (r == 0) t = row_to_all<0>(xb);
+        else if (r == 1) t = row_to_all<1>(xb);
+        else t = row_to_all<2>(xb);
+        if (g > r) xb = fma(-cf[r], t, xb);
+      }
+    }
+    x[B] = xb;
+    if constexpr (B < 3) {
+      f64x4 acc = {x[0], x[1], x[2], x[3]};
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-aop, xb, acc, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = acc[q];
+    }
+    solve16_block<B + 1, F>(x, D, rdg);
+  }
+}
+
+template <bool F = false>
+__device__ __forceinline__ void solve16(double (&x)[4], const double* D, const double* rdg) {
+  solve16_block<0, F>(x, D, rdg);
 }
 
 // ---- Adaptation on matrix cores, for P <= 16 * MAXT (every TestData cell; configs 4/5). One
@@ -1893,8 +1921,8 @@ __device__ __forceinline__ void chol16_finish(double (&a)[4], double* dpiv, doub
 //     v_mfma_f64_16x16x4_f64 products into the owned tiles, merged with (cov, mean, wsum) by the
 //     pairwise-update formula (mcmcstat's row-by-row recurrence in exact arithmetic);
 //   Cholesky cov + qcovadj I = U'U, right-looking by 16-column panels: the owners copy panel row pk
-//     to LDS (the diagonal tile factored on the way, in its owner's registers: chol16_step2),
-//     16-lane groups solve the panel's row tiles (one column per lane), the owners take their U
+//     to LDS (the diagonal tile factored on the way, in its owner's registers: chol16),
+//     one wave per row tile solves the panel (solve16), the owners take their U
 //     tiles back and every trailing tile takes the rank-16 update as 4 MFMAs on its owner's
 //     registers. R = U * adascale, stored only when the
 //     whole factorization succeeded (a singular matrix keeps the previous R, as mcmcstat).
@@ -2167,9 +2195,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
         dt[q] = v;
       }
       bool bad = false;
-      chol16_step2<0, kFresh>(dt, rdg, bad);
-      wave_sync();
-      chol16_finish<kFresh>(dt, rdg, rdg);
+      chol16<kFresh>(dt, rdg, bad);
 #pragma unroll
       for (int q = 0; q < 4; ++q) Bn[256 * pr + (kq + 4 * q) * 16 + row] = dt[q];
       if (bad && lane == 0) fail = 1;
@@ -2186,24 +2212,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
     }
     double* B = Pb + (pk & 1) * NT * 256;  // tile (pk, tj) at B + 256 tj
     const double* D = B + 256 * pk;
-    // (2) the panel's row tiles (pk, tj > pk): U_pk' X = A -> X, one column per lane
-    {
-      const int ln = lane_idx<kFresh>(), row = ln & 15;
-      const int g = w * 4 + (ln >> 4);  // 16-lane group 0 .. 4 NW - 1
-      for (int tj = pk + 1 + g; tj < NT; tj += 4 * NW) {
-        double* A = B + 256 * tj;
-        double x[16];
+    // (2) the panel's row tiles (pk, tj > pk): U_pk' X = A -> X, one tile per wave (solve16)
+    for (int tj = pk + 1 + w; tj < NT; tj += NW) {  // uniform
+      const int ln = lane_idx<kFresh>(), row = ln & 15, kq = ln >> 4;
+      double* A = B + 256 * tj;
+      double x[4];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = A[k * 16 + row];
+      for (int q = 0; q < 4; ++q) x[q] = A[(kq + 4 * q) * 16 + row];
+      solve16<kFresh>(x, D, rdg);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          x[k] = x[k] * rdg[k];
-#pragma unroll
-          for (int m = k + 1; m < 16; ++m) x[m] = fma(-D[k * 16 + m], x[k], x[m]);
-        }
-#pragma unroll
-        for (int k = 0; k < 16; ++k) A[k * 16 + row] = x[k];
-      }
+      for (int q = 0; q < 4; ++q) A[(kq + 4 * q) * 16 + row] = x[q];
     }
     __syncthreads();
     TCI_APHASE(5)
@@ -2259,8 +2277,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
 //     LDS in batches of rb rows (as many as fit 96 KB, a multiple of 4) and accumulates the owned
 //     tiles' scatter with v_mfma_f64_16x16x4_f64, then merges them into (cov, mean, wsum) with
 //     k_adapt_mfma's formula and writes cov + qcovadj I to the tile grid;
-//   Cholesky: per panel pk, wave 0 factors the diagonal tile in registers (chol16_step2), 16-lane
-//     groups solve the panel's row tiles, every wave takes trailing tiles (pk < ti <= tj) round-robin
+//   Cholesky: per panel pk, wave 0 factors the diagonal tile in registers (chol16), one wave
+//     per row tile solves the panel (solve16), every wave takes trailing tiles (pk < ti <= tj) round-robin
 //     and applies the rank-16 update as 4 MFMAs. R = U * adascale, stored only when every pivot
 //     was positive (a singular matrix keeps the previous R, as mcmcstat).
 // The tile arithmetic is k_adapt_mfma's, so both kernels give the same R up to the order of the
@@ -2443,9 +2461,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
       for (int q = 0; q < 4; ++q) dt[q] = A[(kq + 4 * q) * 16 + row];
       bool bad = false;
-      chol16_step2<0>(dt, rdg, bad);
-      wave_sync();
-      chol16_finish(dt, rdg, rdg);
+      chol16(dt, rdg, bad);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         A[(kq + 4 * q) * 16 + row] = dt[q];
@@ -2456,21 +2472,14 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
     __syncthreads();
     TCI_GPHASE(2)
     if (fail) return false;
-    const int g = w * 4 + kq;  // 16-lane group 0 .. 4 NW - 1
-    for (int tj = pk + 1 + g; tj < NT; tj += 4 * NW) {
-      asm volatile("" ::: "memory");  // Dt is re-read per tile, not hoisted into 120 registers
+    for (int tj = pk + 1 + w; tj < NT; tj += NW) {  // one tile per wave (solve16)
       double* A = tile(pk, tj);
-      double x[16];
+      double x[4];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) x[k] = A[k * 16 + row];
+      for (int q = 0; q < 4; ++q) x[q] = A[(kq + 4 * q) * 16 + row];
+      solve16(x, Dt, rdg);
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        x[k] = x[k] * rdg[k];
-#pragma unroll
-        for (int m = k + 1; m < 16; ++m) x[m] = fma(-Dt[k * 16 + m], x[k], x[m]);
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) A[k * 16 + row] = x[k];
+      for (int q = 0; q < 4; ++q) A[(kq + 4 * q) * 16 + row] = x[q];
     }
     __syncthreads();
     TCI_GPHASE(3)
