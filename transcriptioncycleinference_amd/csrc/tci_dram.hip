@@ -856,9 +856,19 @@ __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE)))
     // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
     double* d0 = drow + step0 * DW;
     const auto put = [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; };
+    // WALK's short pass (a 100-step chunk's last: 3 x 32 + 4 steps) runs only the row tiles it fills
+    // -- an instance with fewer tiles, the same products (each depends only on its row of Z and the k
+    // order): config 4 2,381 -> 2,289 us per launch (r05p); the fused engine's 128-VGPR instance
+    // spilled more with it (77.4 -> 78.1 us per TestData chunk) and keeps one instance
     if (!(TCI_DRAWS_ABLATE & 2))
-      for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT)
-        mfma_zr_pf<MT, kDrawCT, kDrawWaves, kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
+      for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT) {
+        if (MT > 2 && 2 * ns <= 16)
+          mfma_zr_pf<1, kDrawCT, kDrawWaves, kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
+        else if (MT > 2 && 2 * ns <= 32)
+          mfma_zr_pf<(MT > 2 ? 2 : MT), kDrawCT, kDrawWaves, kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
+        else
+          mfma_zr_pf<MT, kDrawCT, kDrawWaves, kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
+      }
     for (int k = w; k < ns; k += kDrawWaves) {
       const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
       if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
