@@ -40,6 +40,7 @@
 #include "tci_diag.h"
 #include "tci_dram_internal.h"
 #include "tci_eval.h"
+#include "tci_tile16.h"
 
 namespace tci {
 
@@ -211,13 +212,6 @@ __device__ __forceinline__ double gamma_at(uint64_t seed, int64_t c, int64_t ste
 // Every engine reduces through this one function, so their bits agree.
 __device__ __forceinline__ double wsum64(double x) { return wave_sum(x); }
 
-// Lane l's value of x in every lane (readlane: scalar broadcast, l uniform).
-__device__ __forceinline__ double lane_bcast(double x, int l) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
-  return __hiloint2double(hi, lo);
-}
-
 // Acceptance terms shared by every engine (the same expressions, so the same bits):
 //   log of a Metropolis ratio  -0.5*(ss_new - ss_old)/s2 - 0.5*(prior_new - prior_old), with the
 //   division by s2 taken as a product with the precision ip = 1/s2 (computed once per state);
@@ -327,7 +321,6 @@ __device__ void load_R(double* Rl, const DramState& st, int64_t c, int P) {
 // the triangle. A product depends only on its row of Z and the fixed k order, so every MT/CT
 // instance (the batched engine's 1-row proposals, the fused engine's 32-row draws) gives the same
 // bits.
-typedef double f64x4 __attribute__((ext_vector_type(4)));
 // top: the highest column tile of this call (tiles top, top-1, .. top+1-NWV*CT are computed):
 // (P + 15)/16 - 1 for one call; wider rows loop over tops (propose_block).
 // PF > 0 (R in global memory): every k-step also loads the R values of all CT tiles PF k-steps
@@ -1778,147 +1771,6 @@ int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, 
 }
 
 
-
-// This lane's index computed afresh (v_mbcnt). The adaptation kernels run at their register budget,
-// where the compiler keeps lane-derived indices alive across whole phases and spills them: a scratch
-// reload inside the diagonal factorization or the panel solve puts a memory round trip on a
-// latency-bound path (one per pivot pair, r04 asm). Volatile, so it is recomputed where it is used.
-__device__ __forceinline__ int lane_now() {
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
-}
-
-template <bool F>  // F: lane_now() (a kernel that spills), else threadIdx.x (kept in a register)
-__device__ __forceinline__ int lane_idx() {
-  if constexpr (F) return lane_now();
-  return (int)(threadIdx.x & 63);
-}
-
-// Lane (16 g + K)'s x in every lane of 16-lane row g (DPP row_newbcast, no LDS).
-template <int K>
-__device__ __forceinline__ double row_bcast16(double x) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x150 + K, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x150 + K, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-
-// 16-lane row G's x in every row (lane l gets lane 16 G + (l & 15)): two gfx950 permlane swaps per
-// 32-bit half (permlane32_swap pairs rows {0,1} with {2,3}, permlane16_swap row 0 with 1 and 2
-// with 3), no LDS round trip (ds_bpermute waits on the LDS pipe).
-template <int G>
-__device__ __forceinline__ double row_to_all(double x) {
-  unsigned h[2] = {(unsigned)__double2loint(x), (unsigned)__double2hiint(x)};
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const auto a = __builtin_amdgcn_permlane32_swap(h[q], h[q], false, false);  // [R0 R1 R0 R1], [R2 R3 R2 R3]
-    const unsigned y = G < 2 ? a[0] : a[1];
-    const auto b = __builtin_amdgcn_permlane16_swap(y, y, false, false);        // [Ra Ra Ra Ra], [Rb Rb Rb Rb]
-    h[q] = (G & 1) ? b[1] : b[0];
-  }
-  return __hiloint2double((int)h[1], (int)h[0]);
-}
-
-// Cholesky factorization A = U'U of a symmetric 16 x 16 tile held by ONE wave in registers, in the
-// MFMA accumulator layout (lane 16 g + j holds rows g, g+4, g+8, g+12 of column j: slot q = rows
-// 4q .. 4q+3), blocked by 4 pivots. Block B is slot B: its four pivots K = 4B + r eliminate inside the
-// slot only (rows 4B + g > K of columns j > K take A -= A[.][K] A[K][j] / d, column K a DPP row
-// broadcast, row K a permlane row broadcast), the slot's rows are scaled to U rows (1 / sqrt(d) per
-// row), and the trailing rows and columns >= 4B + 4 take the rank-4 update A -= U_B' U_B as ONE
-// v_mfma_f64_16x16x4 -- the slot itself is both operands (A[i][k] = U[4B+k][i] sits in lane 16 k + i,
-// the B operand's lane for U[4B+k][j]), zeroed in the columns < 4B + 4. The pivot round trip
-// (readlane -> reciprocal -> update) stays on one slot instead of four and 12 of the 15 rank-1
-// updates of the whole tile become 3 MFMAs. rdg[4B + g] = 1 / U[4B+g][4B+g] for the panel solve;
-// bad if a pivot is not positive and finite.
-template <int B, int R, bool F>
-__device__ __forceinline__ void chol16_pivot(double& x, double& dv, bool& bad) {
-  constexpr int K = 4 * B + R;
-  const int lane = lane_idx<F>(), g = lane >> 4, j = lane & 15;
-  const double d = lane_bcast(x, 16 * R + K);  // A[K][K]
-  bad = bad || !(d > 0.0) || !isfinite(d);
-  if (g == R) dv = d;
-  if constexpr (R < 3) {
-    const double akj = row_to_all<R>(x);   // A[K][j]
-    const double aik = row_bcast16<K>(x);  // A[4B + g][K]
-    double rd = __builtin_amdgcn_rcp(d);
-    rd = fma(rd, fma(-d, rd, 1.0), rd);
-    const double sj = akj * rd;
-    if (g > R && j > K) x = fma(-aik, sj, x);
-  }
-}
-
-template <int B, bool F>
-__device__ __forceinline__ void chol16_block(double (&a)[4], double* rdg, bool& bad) {
-  if constexpr (B < 4) {
-    const int lane = lane_idx<F>(), g = lane >> 4, j = lane & 15;
-    double x = a[B], dv = 1.0;
-    chol16_pivot<B, 0, F>(x, dv, bad);
-    chol16_pivot<B, 1, F>(x, dv, bad);
-    chol16_pivot<B, 2, F>(x, dv, bad);
-    chol16_pivot<B, 3, F>(x, dv, bad);
-    const double rs = 1.0 / sqrt(dv);
-    const double u = x * rs;  // U[4B + g][j] for j >= 4B + g
-    if (j == 4 * B + g) rdg[j] = rs;
-    if constexpr (B < 3) {
-      const double op = j >= 4 * B + 4 ? u : 0.0;
-      f64x4 acc = {a[0], a[1], a[2], a[3]};
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-op, op, acc, 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[q] = acc[q];
-    }
-    a[B] = u;
-    chol16_block<B + 1, F>(a, rdg, bad);
-  }
-}
-
-template <bool F = false>
-__device__ __forceinline__ void chol16(double (&a)[4], double* rdg, bool& bad) {
-  chol16_block<0, F>(a, rdg, bad);
-}
-
-// The panel solve U' X = A of one 16 x 16 row tile, held by one wave in the MFMA layout (x[q]: rows
-// g + 4q of column j), U the panel's diagonal tile row-major in LDS (D[k 16 + m] = U[k][m], m >= k)
-// and rdg[k] = 1 / U[k][k]. Blocked like chol16: the four rows of slot B are solved in turn (row r
-// scaled by rdg, broadcast to the slot's later rows by permlanes, fma with U[4B+r][4B+g]), then the
-// rows below take X -= U_B' X_B as one MFMA (A operand: U[4B+k][i] for i >= 4B + 4, B operand: the
-// slot). Every coefficient is an LDS load independent of the recurrence (the 16-lane column loop
-// waited on 136 dependent-order LDS reads).
-template <int B, bool F>
-__device__ __forceinline__ void solve16_block(double (&x)[4], const double* D, const double* rdg) {
-  if constexpr (B < 4) {
-    const int lane = lane_idx<F>(), g = lane >> 4, j = lane & 15;
-    const double rg = rdg[4 * B + g];
-    double cf[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) cf[r] = D[(4 * B + r) * 16 + 4 * B + g];  // U[4B+r][4B+g], used for g > r
-    const double aop = (B < 3 && j >= 4 * B + 4) ? D[(4 * B + g) * 16 + j] : 0.0;
-    double xb = x[B];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (g == r) xb = xb * rg;
-      if (r < 3) {
-        double t;
-        if (r == 0) t = row_to_all<0>(xb);
-        else if (r == 1) t = row_to_all<1>(xb);
-        else t = row_to_all<2>(xb);
-        if (g > r) xb = fma(-cf[r], t, xb);
-      }
-    }
-    x[B] = xb;
-    if constexpr (B < 3) {
-      f64x4 acc = {x[0], x[1], x[2], x[3]};
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-aop, xb, acc, 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) x[q] = acc[q];
-    }
-    solve16_block<B + 1, F>(x, D, rdg);
-  }
-}
-
-template <bool F = false>
-__device__ __forceinline__ void solve16(double (&x)[4], const double* D, const double* rdg) {
-  solve16_block<0, F>(x, D, rdg);
-}
 
 // ---- Adaptation on matrix cores, for P <= 16 * MAXT (every TestData cell; configs 4/5). One
 // workgroup per chain. The upper triangle of cov + qcovadj I is held as 16 x 16 tiles in the MFMA
