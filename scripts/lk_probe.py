@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Price the bench launch's parts (likelihood kernel, 299 cells x 256 proposals): the shipped batch,
 the same batch with every row inactive (wave launch + flag read only), with every row active (the
-bounds-rejected proposals evaluated too), and the in-bounds rows alone, compacted (B = 55k rows)."""
+bounds-rejected proposals evaluated too), the in-bounds rows alone, compacted (B = 55k rows), and the
+same rows with the rejected ones all after (or all before) the in-bounds ones."""
 import json
 import os
 import sys
@@ -23,6 +24,13 @@ act = active.astype(bool)
 cases = {"bench": (theta, cid, active), "all_inactive": (theta, cid, np.zeros_like(active)),
          "all_active": (theta, cid, np.ones_like(active)),
          "compacted": (np.ascontiguousarray(theta[act]), np.ascontiguousarray(cid[act]), np.ones(act.sum(), np.uint8))}
+# the same rows reordered: the in-bounds rows first (their order kept), the rejected rows after them
+order = np.concatenate([np.flatnonzero(act), np.flatnonzero(~act)])
+cases["active_first"] = (np.ascontiguousarray(theta[order]), np.ascontiguousarray(cid[order]),
+                         np.ascontiguousarray(active[order]))
+order2 = np.concatenate([np.flatnonzero(~act), np.flatnonzero(act)])
+cases["inactive_first"] = (np.ascontiguousarray(theta[order2]), np.ascontiguousarray(cid[order2]),
+                           np.ascontiguousarray(active[order2]))
 res = {}
 for name, (th, ci, ac) in cases.items():
     th_d, ci_d, ac_d = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (th, ci, ac))
