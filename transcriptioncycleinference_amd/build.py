@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_ROOT = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 SOURCES = [os.path.join(CSRC, "tci_kernels.hip"), os.path.join(CSRC, "tci_dram.hip"), os.path.join(CSRC, "tci_api.cpp")]
-HEADERS = [os.path.join(REPO_ROOT, "include", "tci.h"), os.path.join(CSRC, "tci_internal.h"), os.path.join(CSRC, "tci_diag.h"), os.path.join(CSRC, "tci_tile16.h"),
+HEADERS = [os.path.join(REPO_ROOT, "include", "tci.h"), os.path.join(CSRC, "tci_internal.h"), os.path.join(CSRC, "tci_diag.h"), os.path.join(CSRC, "tci_tile16.h"), os.path.join(CSRC, "tci_adapt_map.h"),
            os.path.join(CSRC, "tci_dram_internal.h"), os.path.join(CSRC, "tci_eval.h")]
 LIB = os.path.join(PKG_DIR, "libtci.so")
 ARCH = "gfx950"  # CDNA4 only: the kernels use gfx950 instructions (v_bitop3_b32, permlane16/32 swaps)

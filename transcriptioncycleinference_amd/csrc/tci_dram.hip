@@ -41,6 +41,7 @@
 #include "tci_dram_internal.h"
 #include "tci_eval.h"
 #include "tci_tile16.h"
+#include "tci_adapt_map.h"
 
 namespace tci {
 
@@ -1898,14 +1899,19 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
     mb[j] = j < P ? st.wsumv[c * ld + j] / (double)p.adaptint : 0.0;
     mo[j] = j < P ? mu[j] : 0.0;
   }
-  // owned tiles (ti <= tj): every NW-th of the row-major tile order, from w. Slots past the last
-  // tile compute on tile (0, 0) and are discarded, so the code is straight-line and every array
+  // owned tiles (ti <= tj): wave w's slots from kAdMap (tci_adapt_map.h: the diagonal tile a panel
+  // factors goes to a wave with few trailing tiles in the panel before it). Slots past the wave's
+  // last tile compute on tile (0, 0) and are discarded, so the code is straight-line and every array
   // index is a compile-time constant (the tiles stay in registers, no scratch memory).
-  int sti[kAdOwn], stj[kAdOwn];
+  static_assert(NW == 8 && kAdOwn <= kAdMapSlots && MAXT <= kAdMapMaxT, "tile map shape");
+  int sti[kAdOwn], stj[kAdOwn], stk[kAdOwn];  // tile row, column, row-major index (the cov layout)
+  int nown = 0;                               // valid slots (a wave's tiles fill its first slots)
 #pragma unroll
   for (int o = 0; o < kAdOwn; ++o) {
-    int k = w + NW * o, ti = 0;
-    if (k >= T) k = 0;
+    int k = kAdMap[NT - 1][w][o], ti = 0;
+    if (k >= 0) nown = o + 1;  // uniform
+    if (k < 0) k = 0;
+    stk[o] = k;
     while (k >= NT - ti) {  // uniform
       k -= NT - ti;
       ++ti;
@@ -1913,7 +1919,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
     sti[o] = ti;
     stj[o] = ti + k;
   }
-  const int nown = (T - w + NW - 1) / NW;  // valid slots
   // ---- the window's runs of equal rows (window_runs)
   const int M = window_runs<NW, (16 * MAXT + 63) / 64, 4>(win, ld, P, nb, rs, rf, &nrun);
   // ---- scatter of the centred runs on MFMA: sum over runs of len * d d' (A operand: the rows
@@ -1965,7 +1970,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const double na = st.wsum[c], nn = na + (double)p.adaptint;
   const double fcross = na * (double)p.adaptint / nn;
   // cov in the owned-tile layout: tile k (row-major upper-tile order; wave w's slot o is tile
-  // w + NW o) at cvg + 256 k, accumulator entry q of lane l at 64 q + l -- four 512-byte reads per
+  // stk[o]) at cvg + 256 k, accumulator entry q of lane l at 64 q + l -- four 512-byte reads per
   // tile, and a diagonal tile keeps both triangles (the scatter, the update and hence the stored
   // values are symmetric bit for bit: the products and sums of (i, j) and (j, i) are the same)
   const double rn1 = 1.0 / (nn - 1.0);
@@ -1979,7 +1984,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int o = o0 + u;
-        old[u][q] = (o < nown && na > 0.0) ? cvg[256 * (w + NW * o) + 64 * q + ln] : 0.0;
+        old[u][q] = (o < nown && na > 0.0) ? cvg[256 * stk[o] + 64 * q + ln] : 0.0;
       }
 #pragma unroll
     for (int u = 0; u < kAdMG; ++u) {
@@ -2002,7 +2007,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
         } else {
           a = i == j ? 1.0 : 0.0;
         }
-        cvg[256 * (w + NW * o) + 64 * q + ln] = cv;
+        cvg[256 * stk[o] + 64 * q + ln] = cv;
         acc[o][q] = a;
       }
     }
