@@ -686,11 +686,14 @@ def test_gpu_chains_follow_the_cpu_restatement(lk, c_oracle, construct, engine):
 # 8-wave adaptation kernel: (chains, points per cell, construct, data seed).
 #   config4: N = 200, P = 207, the built-in construct -- k_adapt_mfma<8, 13>, WALK / FUSED / batched;
 #   config5: N = 200, the two-segment 3x-length construct (BASELINE config 5);
-#   long:    N = 210, P = 217 > 208 -- the generic adaptation kernel k_adapt_gt.
+#   long:    N = 210, P = 217 > 208 -- the generic adaptation kernel k_adapt_gt;
+#   mid:     N = 145 / 160 / 180 (P = 152 / 167 / 187: 10, 11 and 12 tiles per dimension), the tile
+#            ownership maps of k_adapt_mfma<8, 13> no BASELINE config reaches (tci_adapt_map.h).
 RESTATEMENT_SHAPES = {
     "config4": (24, 200, "builtin", 20201028),
     "config5": (16, 200, "two_segment", 20201029),
     "long": (8, 210, "builtin", 20201030),
+    "mid": (4, (145, 160, 180), "builtin", 20201031),
 }
 _restatement_cache = {}
 
@@ -713,7 +716,16 @@ def _restatement_case(shape, c_oracle):
         with Likelihood(from_lists([(t, a, a) for t, a in zip(times, nan)]), cs, device=0) as L:
             return L.forward(theta, np.arange(len(times), dtype=np.int32), grid="interp")
 
-    cells, _ = synthetic_cells(n_cells, n_points, seed, fwd)
+    if isinstance(n_points, tuple):  # n_cells cells of each length
+        parts = []
+        for i, npts in enumerate(n_points):
+            cc, _ = synthetic_cells(n_cells, npts, seed + 7919 * i, fwd)
+            o_ = cc.offsets
+            parts += [(cc.t[o_[k]:o_[k + 1]], cc.ms2[o_[k]:o_[k + 1]], cc.pp7[o_[k]:o_[k + 1]]) for k in range(n_cells)]
+        cells = from_lists(parts, f"synthetic-mixed-{shape}")
+        n_cells = len(parts)
+    else:
+        cells, _ = synthetic_cells(n_cells, n_points, seed, fwd)
     plan = plan_fit(cells, list(range(n_cells)), 5)
     o = DramOptions(n_steps=700, burnintime=300, adaptint=100, stats_from=200, thin=1, seed=91)
     keys = np.array(plan.cells, np.int64)
@@ -730,7 +742,7 @@ def test_gpu_chains_follow_the_cpu_restatement_at_config_shapes(c_oracle, shape,
     """As test_gpu_chains_follow_the_cpu_restatement, at the shapes BASELINE configs 4/5 run
     (TranscriptionCycleMCMC.m:263-273): 700 steps, burn-in scaling at rows 100-300, then four covariance
     updates (rows 400-700) on the P <= 208 matrix-core adaptation (k_adapt_mfma<8, 13>) or, for P = 217,
-    on k_adapt_gt; every engine. Same accept / reject decision at every step; rows, s2chain, summaries
+    on k_adapt_gt, and on cells of 10-12 tiles per dimension (the "mid" shape); every engine. Same accept / reject decision at every step; rows, s2chain, summaries
     and the final proposal factor R within 1e-9."""
     from transcriptioncycleinference_amd import Likelihood
     from transcriptioncycleinference_amd.mcmc import dram_run
@@ -741,7 +753,9 @@ def test_gpu_chains_follow_the_cpu_restatement_at_config_shapes(c_oracle, shape,
         g = dram_run(L, np.array(plan.cells, np.int32), plan.x0, plan.lower, plan.upper, plan.prior_mu,
                      plan.prior_sig, plan.qcov_diag, 1.0, o, chain_keys=keys, want_qcov=True)
     n = cells.lengths[plan.cells]
-    assert int(7 + n.max()) == {"config4": 207, "config5": 207, "long": 217}[shape]
+    assert int(7 + n.max()) == {"config4": 207, "config5": 207, "long": 217, "mid": 187}[shape]
+    if shape == "mid":
+        assert sorted(set(((7 + n + 15) // 16).tolist())) == [10, 11, 12]
     for k in range(len(plan.cells)):
         P = 7 + int(n[k])
         G, Cc = g.chain[:, k, :P], c["chain"][:, k, :P]
