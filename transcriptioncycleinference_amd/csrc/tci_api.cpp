@@ -707,6 +707,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(wacc2, double, n * L);
   TCI_ALLOC(s2acc, double, n * 3);
   TCI_ALLOC(s2log, double, n * (size_t)win);
+  TCI_ALLOC(runf, uint8_t, n * (size_t)win);
   TCI_ALLOC(prop1, double, n * L);
   TCI_ALLOC(prop2, double, n * L);
   TCI_ALLOC(act1, uint8_t, n);

@@ -608,14 +608,28 @@ __global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* _
 // window's logs back at its end (window_records, window_s2_records). (Summing the s2 log at the
 // window's end in k_chain too: 226.9 -> 228.4 us per chunk, r04j.)
 __device__ __forceinline__ int64_t log_slot(const DramParams& p, int64_t row) { return (row - 1) % p.win; }
+// Whether the row in `slot` differs from the chain row before it (any entry unequal, NaN included):
+// the adaptation's runs of equal rows (window_runs), recorded by the engines as they decide the rows
+// instead of re-read and compared by the adaptation.
+__device__ __forceinline__ void log_run(const DramState& st, const DramParams& p, int64_t c, int64_t slot, bool f) {
+  st.runf[c * p.win + slot] = f ? 1 : 0;
+}
 
 // The batched engine's per-step log (one workgroup per chain).
 __device__ void log_row_block(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P, const double* th,
                               double s2) {
   const int64_t slot = log_slot(p, row);
   double* w = st.window + (c * p.win + slot) * st.ld;
-  for (int j = threadIdx.x; j < P; j += kThreads) w[j] = th[j];
-  if (threadIdx.x == 0) st.s2log[c * p.win + slot] = s2;
+  int d = slot == 0;  // a window's first row starts a run
+  for (int j = threadIdx.x; j < P; j += kThreads) {
+    if (slot > 0) d |= !(w[j - st.ld] == th[j]);  // the row before it, logged by the previous step
+    w[j] = th[j];
+  }
+  d = __syncthreads_or(d);
+  if (threadIdx.x == 0) {
+    st.s2log[c * p.win + slot] = s2;
+    log_run(st, p, c, slot, d != 0);
+  }
 }
 
 struct S2Stats {
@@ -909,6 +923,14 @@ __device__ __forceinline__ void log_row(const DramState& st, const DramParams& p
 }
 __device__ __forceinline__ void log_s2(const DramState& st, const DramParams& p, int64_t c, int64_t slot, double s2) {
   st.s2log[c * p.win + slot] = s2;
+}
+// any(x != y) over a chain row held one entry per lane and k (NJ entries, j = lane + 64 k < P)
+template <int NJ>
+__device__ __forceinline__ bool row_differs(const double* x, const double* y, int P, int lane) {
+  uint64_t d = 0;
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) d |= wave_ballot(lane + 64 * k < P && !(x[k] == y[k]));
+  return d != 0;
 }
 
 // Pairwise merge of a batch (nb values, shifted sums S1, S2 about K) into running (n, mean, M2).
@@ -1238,8 +1260,9 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   const bool keep_rows = (st.chain_out != nullptr || st.s2_out != nullptr) && p.thin > 0;
   int64_t kkeep = keep_rows ? (s_begin - 1 + p.thin - 1) / p.thin : 0;
   int64_t next_keep = keep_rows ? kkeep * p.thin + 1 : INT64_MAX;
-  auto rec_row = [&](int64_t row, const double* x) {  // kRecWave
+  auto rec_row = [&](int64_t row, const double* x, bool f) {  // kRecWave; f: x differs from the row before
     double* wr = wlog + (int)(slot0 + row) * ldi;
+    if (lane == 0) log_run(st, p, c, slot0 + row, f);
 #pragma unroll
     for (int k = 0; k < NJ; ++k)
       if (lane + 64 * k < P) wr[lane + 64 * k] = x[k];
@@ -1265,10 +1288,13 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   };
   auto flush_vec = [&]() {  // unrolled: a bounded store count (a runtime loop made the compiler
                             // wait for every store before the next round's loads were used)
+    // the round's unmoved rows repeat the state before it (thp, as did the row before them); its last
+    // row is the state after it
+    const bool mv = padv >= 1 && row_differs<NJ>(th, thp, P, lane);
 #pragma unroll
     for (int i = 0; i < D - 1; ++i)
-      if (i + 1 < padv) rec_row(prow + i, thp);  // uniform
-    if (padv >= 1) rec_row(prow + padv - 1, th);
+      if (i + 1 < padv) rec_row(prow + i, thp, false);  // uniform
+    if (padv >= 1) rec_row(prow + padv - 1, th, mv);
   };
   auto flush_s2 = [&](double x0) {
 #pragma unroll
@@ -1631,9 +1657,12 @@ __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu
   };
   // the records of row r (the chain state th, s2 after it): the window log, the window sums in LDS
   // and the thinned outputs
-  auto record_row = [&](int64_t r) {
+  auto record_row = [&](int64_t r, bool f) {  // f: th differs from the row before
     log_row<NJ>(st, p, c, slot0 + r, P, th, lane);
-    if (lane == 0) log_s2(st, p, c, slot0 + r, s2);
+    if (lane == 0) {
+      log_s2(st, p, c, slot0 + r, s2);
+      log_run(st, p, c, slot0 + r, f);
+    }
     int64_t kk;
     const bool keep = st.chain_out != nullptr && kept_row(p, r, kk);
 #pragma unroll
@@ -1653,13 +1682,14 @@ __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu
   // row decided by the previous step, recorded after this step's loads are issued (its latency
   // hides the records: config 4 2,230 -> 2,178 us per chunk against recording it at once, r04wearly)
   int64_t prow = s_begin - 1;
+  bool pmv = false;  // row prow differs from the row before it
   for (int64_t s = s_begin; s <= s_end; ++s) {
     launder_lane(lane);
     double u[NJ];
     load_u(u, s, 0);
     const double* sc = drow + s * DW + 2 * ld;
     const double q1 = sc[D_Q1], U1 = sc[D_U1], U2 = sc[D_U2], G = sc[D_G];
-    if (prow >= s_begin) record_row(prow);
+    if (prow >= s_begin) record_row(prow, pmv);
     double r1, pr1, r2 = INFINITY, pr2 = 0.0;
     const bool inb1 = evaluate(u, 1.0, r1, pr1);
     // a12 (k_chain lane 0): ssA = r1 (+Inf out of bounds), prA = pr1 (0 out of bounds)
@@ -1681,9 +1711,14 @@ __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu
         acc2 = dram_dr_accept(U2, a12, a32, l2, q1);
       }
     }
+    bool mv = false;
     if (acc || acc2) {  // the accepted proposal is the last one evaluated: it is in yb
+      double yn[NJ];
 #pragma unroll
-      for (int k = 0; k < NJ; ++k) th[k] = yb[lane + 64 * k];
+      for (int k = 0; k < NJ; ++k) yn[k] = yb[lane + 64 * k];
+      mv = row_differs<NJ>(yn, th, P, lane);
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) th[k] = yn[k];
       ss = acc ? r1 : r2;
       prior = acc ? pr1 : pr2;
       nacc += 1;
@@ -1694,8 +1729,9 @@ __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu
     if (p.updatesigma) s2 = 1.0 / (G * (2.0 / ss));
     wave_sync();  // yb reads are done before the next evaluation rewrites it
     prow = s;  // recorded under the next step's loads
+    pmv = mv;
   }
-  if (prow >= s_begin) record_row(prow);
+  if (prow >= s_begin) record_row(prow, pmv);
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
     const int j = lane + 64 * k;
@@ -1796,47 +1832,18 @@ int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, 
 // repeats the row before it, which adds the same outer product to the scatter again, so the
 // scatter runs once per run, weighted by its length -- about 1 + 100 x the acceptance rate of the
 // 100 rows; the same sum in exact arithmetic, rounded differently from row-by-row sums (and the
-// same in every engine). Wave w of NW compares rows w, w + NW, .. with their predecessors (any
-// entry unequal, NaN included: a new run), RU rows' loads in flight together, over every column
-// (blocks of 64 NJA; one block while P <= 64 NJA); wave 0 then lists the run starts in row order.
-// rs[0..m) = start rows, rs[m] = nb; rf: nb ints of LDS scratch.
-template <int NW, int NJA, int RU>
-__device__ int window_runs(const double* win, int64_t ld, int P, int nb, int* rs, int* rf, int* nrun) {
+// same in every engine). A row starts a run when it is the window's first or differs from the row
+// before it (any entry unequal, NaN included) -- the engines record that flag as they log the row
+// (DramState::runf; re-reading and comparing the window's rows here took 38k of the 261k cycles of
+// a config-4 adaptation, profiles/r05/r05y_aprof4.json). Wave 0 lists the run starts in row order:
+// rs[0..m) = start rows, rs[m] = nb.
+__device__ int window_runs(const uint8_t* runf, int nb, int* rs, int* nrun) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  for (int r0 = w; r0 < nb; r0 += RU * NW) {  // uniform per wave
-    bool d[RU];
-#pragma unroll
-    for (int u = 0; u < RU; ++u) d[u] = r0 + u * NW == 0;
-    for (int j0 = 0; j0 < P; j0 += 64 * NJA) {  // uniform
-      double a[RU][NJA], b[RU][NJA];
-#pragma unroll
-      for (int u = 0; u < RU; ++u) {
-        const int r = min(r0 + u * NW, nb - 1), rp = max(r - 1, 0);
-#pragma unroll
-        for (int k = 0; k < NJA; ++k) {
-          const int j = min(j0 + lane + 64 * k, P - 1);
-          a[u][k] = win[(int64_t)r * ld + j];
-          b[u][k] = win[(int64_t)rp * ld + j];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < RU; ++u)
-#pragma unroll
-        for (int k = 0; k < NJA; ++k) d[u] = d[u] || !(a[u][k] == b[u][k]);
-    }
-#pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int r = r0 + u * NW;
-      const bool any = wave_ballot(d[u]) != 0;
-      if (lane == 0 && r < nb) rf[r] = any ? 1 : 0;
-    }
-  }
-  __syncthreads();
   if (w == 0) {  // run starts in row order (a ballot prefix per 64 rows)
     int m = 0;
     for (int r0 = 0; r0 < nb; r0 += 64) {
       const int r = r0 + lane;
-      const bool f = r < nb && rf[r] != 0;
+      const bool f = r < nb && (r == 0 || runf[r] != 0);
       const uint64_t bal = wave_ballot(f);
       if (f) rs[m + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0))] = r;
       m += __builtin_popcountll(bal);
@@ -1891,7 +1898,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const double* win = st.window + c * p.win * ld;
   int* rs = (int*)(mo + LX);  // [nb + 1] the window's runs of equal rows: start rows, then nb
   int* rf = rs + nb + 1;      // [nb] 1 where a run starts
-  uint64_t aph[6] = {0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
+  uint64_t aph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
 #define TCI_APHASE(k) \
   if (TCI_ADAPT_PROFILE) { a1 = stamp(); aph[k] += a1 - a0; a0 = a1; }
   // ---- batch mean from the window's column sums (kept by the engines as rows are recorded)
@@ -1920,7 +1927,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
     stj[o] = ti + k;
   }
   // ---- the window's runs of equal rows (window_runs)
-  const int M = window_runs<NW, (16 * MAXT + 63) / 64, 4>(win, ld, P, nb, rs, rf, &nrun);
+  const int M = window_runs(st.runf + c * p.win, nb, rs, &nrun);
+  TCI_APHASE(6)
   // ---- scatter of the centred runs on MFMA: sum over runs of len * d d' (A operand: the rows
   //      times their lengths, B: the rows); batch m0 + kAdRB is loaded while m0 is multiplied
   f64x4 acc[kAdOwn];
@@ -2131,7 +2139,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   TCI_APHASE(4)
 #undef TCI_APHASE
   if (TCI_ADAPT_PROFILE && t == 0 && st.prof != nullptr)
-    for (int q = 0; q < 6; ++q) atomicAdd((unsigned long long*)&st.prof[q], (unsigned long long)aph[q]);
+    for (int q = 0; q < 8; ++q) atomicAdd((unsigned long long*)&st.prof[q], (unsigned long long)aph[q]);
   if (t == 0) st.nrej_win[c] = 0;
 }
 
@@ -2216,7 +2224,7 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
   const double na = st.wsum[c], nn = na + (double)p.adaptint;
   const double fcross = na * (double)p.adaptint / nn;
   const double rn1 = 1.0 / (nn - 1.0);
-  const int M = window_runs<NW, 9, 1>(win, ld, P, nb, rs, rf, &nrun);  // any P (blocks of 576 columns)
+  const int M = window_runs(st.runf + c * p.win, nb, rs, &nrun);
   // ---- covupd: scatter of the centred window runs (each row once, times its run length) + merge,
   //      kGtTiles tiles per wave and pass
   for (int base = 0; base < T; base += NW * kGtTiles) {

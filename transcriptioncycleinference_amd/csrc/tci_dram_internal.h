@@ -50,6 +50,8 @@ struct DramState {
   double* window;          // chain rows by window slot (DramParams::win per chain): the covupd window, and
                            // every engine's per-row log (k_stats)
   double* s2log;           // s2 of each row of the window, by window slot
+  uint8_t* runf;           // 1 where a window row differs from the chain row before it (a new run of equal
+                           // rows: the adaptation scatters each run once), by window slot
   double* wsumv;           // column sums of the window's rows (row order; the adaptation's batch mean); during a
                            // window that spans k_chain launches, its running sums so far with
   double* wacc1;           //   the shifted sums S1, S2 of the statistics rows (n_chains x ld)
