@@ -608,27 +608,23 @@ __global__ __launch_bounds__(kThreads) void k_init(DramState st, const double* _
 // window's logs back at its end (window_records, window_s2_records). (Summing the s2 log at the
 // window's end in k_chain too: 226.9 -> 228.4 us per chunk, r04j.)
 __device__ __forceinline__ int64_t log_slot(const DramParams& p, int64_t row) { return (row - 1) % p.win; }
-// Whether the row in `slot` differs from the chain row before it (any entry unequal, NaN included):
-// the adaptation's runs of equal rows (window_runs), recorded by the engines as they decide the rows
-// instead of re-read and compared by the adaptation.
+// Whether the step that made the row in `slot` moved the chain (accepted a proposal): the
+// adaptation's runs of equal rows (window_runs), recorded by the engines as they decide the rows
+// instead of re-read and compared by the adaptation. (An accepted proposal equal to the state in
+// every entry would split a run in two: the same sum in exact arithmetic.)
 __device__ __forceinline__ void log_run(const DramState& st, const DramParams& p, int64_t c, int64_t slot, bool f) {
   st.runf[c * p.win + slot] = f ? 1 : 0;
 }
 
 // The batched engine's per-step log (one workgroup per chain).
 __device__ void log_row_block(const DramState& st, const DramParams& p, int64_t c, int64_t row, int P, const double* th,
-                              double s2) {
+                              double s2, bool moved) {
   const int64_t slot = log_slot(p, row);
   double* w = st.window + (c * p.win + slot) * st.ld;
-  int d = slot == 0;  // a window's first row starts a run
-  for (int j = threadIdx.x; j < P; j += kThreads) {
-    if (slot > 0) d |= !(w[j - st.ld] == th[j]);  // the row before it, logged by the previous step
-    w[j] = th[j];
-  }
-  d = __syncthreads_or(d);
+  for (int j = threadIdx.x; j < P; j += kThreads) w[j] = th[j];
   if (threadIdx.x == 0) {
     st.s2log[c * p.win + slot] = s2;
-    log_run(st, p, c, slot, d != 0);
+    log_run(st, p, c, slot, moved);
   }
 }
 
@@ -649,7 +645,7 @@ __global__ __launch_bounds__(kThreads) void k_init_stats(DramState st, DramParam
     st.sq_mean[c] = 0.0;
     st.sq_m2[c] = 0.0;
   }
-  log_row_block(st, p, c, 1, P, st.theta + c * st.ld, st.sigma2[c]);  // chain row 1: the initial state
+  log_row_block(st, p, c, 1, P, st.theta + c * st.ld, st.sigma2[c], true);  // chain row 1: the initial state
   // k_chain's running sums of the first window after row 1 (ColAcc / S2Acc::add of row 1, K = row 1)
   const bool in_stats = p.stats_from <= 1;
   for (int j = threadIdx.x; j < P; j += kThreads) {
@@ -761,7 +757,7 @@ __global__ __launch_bounds__(kThreads) void k_accept2(DramState st, DramParams p
     if (p.updatesigma) st.sigma2[c] = 1.0 / gamma_at(p.seed, st.key[c], step, 0.5 * (double)st.nobs[c], 2.0 / st.ss[c]);
   }
   __syncthreads();
-  log_row_block(st, p, c, step, P, st.theta + c * st.ld, st.sigma2[c]);
+  log_row_block(st, p, c, step, P, st.theta + c * st.ld, st.sigma2[c], st.acc1[c] != 0 || acc2);
 }
 
 __global__ void k_step_incr(int64_t* step) {
@@ -924,14 +920,7 @@ __device__ __forceinline__ void log_row(const DramState& st, const DramParams& p
 __device__ __forceinline__ void log_s2(const DramState& st, const DramParams& p, int64_t c, int64_t slot, double s2) {
   st.s2log[c * p.win + slot] = s2;
 }
-// any(x != y) over a chain row held one entry per lane and k (NJ entries, j = lane + 64 k < P)
-template <int NJ>
-__device__ __forceinline__ bool row_differs(const double* x, const double* y, int P, int lane) {
-  uint64_t d = 0;
-#pragma unroll
-  for (int k = 0; k < NJ; ++k) d |= wave_ballot(lane + 64 * k < P && !(x[k] == y[k]));
-  return d != 0;
-}
+
 
 // Pairwise merge of a batch (nb values, shifted sums S1, S2 about K) into running (n, mean, M2).
 __device__ __forceinline__ void stats_merge(double na, double nb, double K, double S1, double S2, double& mean,
@@ -1205,6 +1194,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   int64_t nev = st.nevals[c];
   int64_t prow = 0;  // rows prow .. prow + padv - 1 were decided by the previous round (logs pending);
   int padv = 0;      // all but the last did not move the chain (their state is thp)
+  bool pmov = false;  // the last of them moved the chain
   // Loads one round ahead. The next round starts at step s + 1 .. s + D, so a round loads every
   // candidate at its START (this wave's offsets of rows s + a1 + 1 .. s + a1 + D + 2 (EPW - 1), and the scalar
   // draws of rows s + 1 .. s + 2D - 1) and the next round picks its rows: a whole round hides the
@@ -1260,7 +1250,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   const bool keep_rows = (st.chain_out != nullptr || st.s2_out != nullptr) && p.thin > 0;
   int64_t kkeep = keep_rows ? (s_begin - 1 + p.thin - 1) / p.thin : 0;
   int64_t next_keep = keep_rows ? kkeep * p.thin + 1 : INT64_MAX;
-  auto rec_row = [&](int64_t row, const double* x, bool f) {  // kRecWave; f: x differs from the row before
+  auto rec_row = [&](int64_t row, const double* x, bool f) {  // kRecWave; f: the row's step moved the chain
     double* wr = wlog + (int)(slot0 + row) * ldi;
     if (lane == 0) log_run(st, p, c, slot0 + row, f);
 #pragma unroll
@@ -1288,13 +1278,11 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   };
   auto flush_vec = [&]() {  // unrolled: a bounded store count (a runtime loop made the compiler
                             // wait for every store before the next round's loads were used)
-    // the round's unmoved rows repeat the state before it (thp, as did the row before them); its last
-    // row is the state after it
-    const bool mv = padv >= 1 && row_differs<NJ>(th, thp, P, lane);
+    // the round's unmoved rows repeat the state before it; its last row moved the chain or not (pmov)
 #pragma unroll
     for (int i = 0; i < D - 1; ++i)
       if (i + 1 < padv) rec_row(prow + i, thp, false);  // uniform
-    if (padv >= 1) rec_row(prow + padv - 1, th, mv);
+    if (padv >= 1) rec_row(prow + padv - 1, th, pmov);
   };
   auto flush_s2 = [&](double x0) {
 #pragma unroll
@@ -1412,6 +1400,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     }
     TCI_PHASE(4)
     int adv = 0;
+    bool rmov = false;
 #pragma unroll
     for (int hh = 0; hh < D; ++hh) {  // uniform
       if (hh >= 1 && s + hh > s_end) break;
@@ -1439,6 +1428,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
         ss = acc ? x1[0] : x2[0];
         prior = acc ? x1[1] : x2[1];  // an accepted candidate was in bounds
         nacc += 1;
+        rmov = true;
         break;  // step s + hh + 1 must be re-proposed around the new state
       }
       nrej += 1;
@@ -1446,6 +1436,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     // the rows s .. s + adv - 1 are recorded next round (s2 of the last: 1/(G*(2/ss)), ss after it)
     prow = s;
     padv = adv;
+    pmov = rmov;
     Gl = lane_bcast(dsc, sbase + 4 * (adv - 1) + D_G);
     gpend = p.updatesigma != 0;
     TCI_PHASE(6)
@@ -1657,7 +1648,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu
   };
   // the records of row r (the chain state th, s2 after it): the window log, the window sums in LDS
   // and the thinned outputs
-  auto record_row = [&](int64_t r, bool f) {  // f: th differs from the row before
+  auto record_row = [&](int64_t r, bool f) {  // f: the step moved the chain
     log_row<NJ>(st, p, c, slot0 + r, P, th, lane);
     if (lane == 0) {
       log_s2(st, p, c, slot0 + r, s2);
@@ -1682,7 +1673,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu
   // row decided by the previous step, recorded after this step's loads are issued (its latency
   // hides the records: config 4 2,230 -> 2,178 us per chunk against recording it at once, r04wearly)
   int64_t prow = s_begin - 1;
-  bool pmv = false;  // row prow differs from the row before it
+  bool pmv = false;  // the step of row prow moved the chain
   for (int64_t s = s_begin; s <= s_end; ++s) {
     launder_lane(lane);
     double u[NJ];
@@ -1711,14 +1702,10 @@ __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu
         acc2 = dram_dr_accept(U2, a12, a32, l2, q1);
       }
     }
-    bool mv = false;
+    const bool mv = acc || acc2;
     if (acc || acc2) {  // the accepted proposal is the last one evaluated: it is in yb
-      double yn[NJ];
 #pragma unroll
-      for (int k = 0; k < NJ; ++k) yn[k] = yb[lane + 64 * k];
-      mv = row_differs<NJ>(yn, th, P, lane);
-#pragma unroll
-      for (int k = 0; k < NJ; ++k) th[k] = yn[k];
+      for (int k = 0; k < NJ; ++k) th[k] = yb[lane + 64 * k];
       ss = acc ? r1 : r2;
       prior = acc ? pr1 : pr2;
       nacc += 1;
@@ -1832,8 +1819,8 @@ int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, 
 // repeats the row before it, which adds the same outer product to the scatter again, so the
 // scatter runs once per run, weighted by its length -- about 1 + 100 x the acceptance rate of the
 // 100 rows; the same sum in exact arithmetic, rounded differently from row-by-row sums (and the
-// same in every engine). A row starts a run when it is the window's first or differs from the row
-// before it (any entry unequal, NaN included) -- the engines record that flag as they log the row
+// same in every engine). A row starts a run when it is the window's first or its step moved the
+// chain -- the engines record that flag as they log the row
 // (DramState::runf; re-reading and comparing the window's rows here took 38k of the 261k cycles of
 // a config-4 adaptation, profiles/r05/r05y_aprof4.json). Wave 0 lists the run starts in row order:
 // rs[0..m) = start rows, rs[m] = nb.
