@@ -1551,10 +1551,12 @@ __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu
   const int64_t DW = draw_stride(ld);
   const double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
   const double inv_ds = 1.0 / p.drscale;
-  // Bounds and prior vectors: held in registers for one segment per dye; re-read from global
-  // memory at every evaluation for NSEG >= 2, whose larger evaluation spilled 108 B per lane at
-  // the 2-waves/SIMD budget (config 5: 230 -> 206 ms per 1000 steps; config 4 unchanged).
-  constexpr bool kGB = NSEG >= 2;
+  // Bounds and prior vectors: held in registers for up to two segments per dye; re-read from
+  // global memory at every evaluation for NSEG >= 3, whose larger evaluation spills at the
+  // 2-waves/SIMD budget. (Round 3 re-read them for NSEG = 2 too, when its evaluation spilled 108 B
+  // per lane; with round 4-5's shorter evaluation NSEG = 2 fits 256 VGPRs without a spill and
+  // holding them took config 5's walk from 3,150 to 2,521 us per launch, bitwise equal, r05gb.)
+  constexpr bool kGB = NSEG >= 3;
   double th[NJ], lo[NJ], hi[NJ], mu[NJ], sg[NJ];
 #pragma unroll
   for (int k = 0; k < NJ; ++k) {
