@@ -1158,7 +1158,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   const int64_t DW = draw_stride(ld);
   // this chain's draws rows (row of step s at (s - s_begin) * DW) and window logs (slot r at r * ld):
   // 32-bit offsets from per-chain bases, no 64-bit multiplies in the loop -- tci_dram_run checks that
-  // chunk * draw_stride(ld) and adaptint * ld fit in an int (the draws buffer's 2 GiB cap bounds the
+  // chunk * draw_stride(ld) and adaptint * ld fit in an int (the draws buffer's GiB cap bounds the
   // first for every chain count)
   const double* const dchain = st.draws + c * p.chunk * DW;
   double* const wlog = st.window + c * p.win * ld;

@@ -19,9 +19,12 @@ constexpr int64_t dram_cov_stride(int64_t ld) {
   return ld * ld > (ld + 15) / 16 * ((ld + 15) / 16 + 1) / 2 * 256 ? ld * ld : (ld + 15) / 16 * ((ld + 15) / 16 + 1) / 2 * 256;
 }
 
-// The fused engine's draws buffer: at most this many GiB (sets the chunk length; an 8 GiB buffer
-// measured within noise, r04s).
-constexpr int64_t kDrawsGiB = 2;
+// The fused engines' draws buffer: at most this many GiB (sets the chunk length). 4 GiB holds a whole
+// 100-step window of configs 4/5's 10,000 chains (2 GiB split it into two 50-step chunks, whose
+// second draws pass filled 36 of its 64 rows): config 4 127.5 -> 123.8 us per step, config 5 135.8
+// -> 131.9, bitwise equal (r05dg; round 4's 8 GiB test predates the short-pass draws and measured
+// within noise, r04s).
+constexpr int64_t kDrawsGiB = 4;
 // Rows longer than this adapt with k_adapt_gt (tiles in global memory); k_adapt_mfma<8, 13, 12> up to
 // here (k_adapt_gt at config 4's P = 207: 5,207 -> 5,887 us, r04q).
 constexpr int64_t kAdaptGtFrom = 208;
