@@ -53,8 +53,6 @@ struct DramState {
   double* window;          // chain rows by window slot (DramParams::win per chain): the covupd window, and
                            // every engine's per-row log (k_stats)
   double* s2log;           // s2 of each row of the window, by window slot
-  uint8_t* runf;           // 1 where a window row differs from the chain row before it (a new run of equal
-                           // rows: the adaptation scatters each run once), by window slot
   double* wsumv;           // column sums of the window's rows (row order; the adaptation's batch mean); during a
                            // window that spans k_chain launches, its running sums so far with
   double* wacc1;           //   the shifted sums S1, S2 of the statistics rows (n_chains x ld)
@@ -83,6 +81,8 @@ struct DramState {
   int64_t* step;           // current chain row (1-based), advanced on device after each step
   int64_t* prof;           // TCI_CHAIN_PROFILE builds only: k_chain phase cycles, summed over chains
   double* draws;           // fused engine: per chain, p.chunk rows of draw_stride(ld) doubles (k_draws)
+  uint8_t* runf;           // 1 where a window row's step moved the chain (a new run of equal rows: the
+                           // adaptation scatters each run once), by window slot
 };
 
 // One chain row's state-independent draws (fused engine): u1 = z1*R [ld], u2 = z2*R [ld], then
