@@ -1,6 +1,6 @@
 // tci_diag.h -- the diagnostics switches of the HIP kernels, in one place. Every one defaults to 0
 // (the product build); a non-zero value is set only by a measurement build (hipcc -D..., see
-// scripts/ab.py) and is never shipped. Ablations produce WRONG results on purpose: they remove work
+// scripts/ab_variants.py) and is never shipped. Ablations produce WRONG results on purpose: they remove work
 // to price it; profiles add s_memtime stamps and atomics.
 #pragma once
 
@@ -18,7 +18,8 @@
 #define TCI_ADAPT_ABLATE 0
 #endif
 // s_memtime cycles per phase into DramState::prof, printed by tci_dram_run: k_chain (1: wave 0's
-// phases, 2: per-wave barrier waits, 3: every wave's phases) / k_adapt_mfma and k_adapt_gt (1).
+// phases, 2: per-wave barrier waits, 3: every wave's phases) / k_adapt_mfma and k_adapt_gt (1:
+// thread 0's phases; k_adapt_mfma's slot 6 is the run listing, window_runs).
 #ifndef TCI_CHAIN_PROFILE
 #define TCI_CHAIN_PROFILE 0
 #endif
