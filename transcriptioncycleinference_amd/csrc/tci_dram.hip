@@ -803,7 +803,9 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
   }
 }
 
-constexpr int kDrawsWPE = 4;             // waves per SIMD k_draws is compiled for (<= 128 VGPRs)
+constexpr int kDrawsWPE = 3;             // waves per SIMD k_draws is compiled for (<= 168 VGPRs): at 4
+                                          // (128 VGPRs) it spilled 34 VGPRs, 76.9 -> 75.5 us per TestData
+                                          // chunk at 3 (r05dw; three 37 KB workgroups per CU)
 constexpr int kDrawsPF = 2;               // R values prefetched this many k-steps ahead (mfma_zr PF)
 constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each), 4-wave workgroups
 enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
@@ -1763,8 +1765,8 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
                    int with_records, hipStream_t stream) {
   const bool wide = p.walk != 0 && draws_walk_wide(st.ld);  // WALK: 64-row draws passes (k_draws<8, 2, 4, 2>)
   const size_t lds = (size_t)draws_lds_bytes(st.ld, wide ? kDrawMTWalk : kDrawMT);
-  // 4-wave workgroups, 2 column tiles x 2 row tiles per wave and MFMA call (128 VGPRs: four
-  // workgroups per CU). Config 4 (WALK, P = 207): 72.7 ms per 1,000 steps with the 8-wave, 2-tile
+  // 4-wave workgroups, 2 column tiles x 2 row tiles per wave and MFMA call (168 VGPRs: three
+  // workgroups per CU, kDrawsWPE). Config 4 (WALK, P = 207): 72.7 ms per 1,000 steps with the 8-wave, 2-tile
   // form -> 53.6 (3 tiles: 58.0, 5: 56.4); TestData (FUSED): 105.3 -> 99.8 us per chunk against
   // 3 tiles (r03t4, r03u); the pipelined z*R loop (mfma_zr_pf) 97.6 -> 86.5 (r04g).
   auto kd = wide ? k_draws<8, 2, kDrawMTWalk, 2> : k_draws<4, 2>;
