@@ -48,4 +48,37 @@ for name, (th, ci, ac) in cases.items():
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1) / 40 * 1e3)
     res[name] = {"rows": len(ci), "active": int(ac.sum()), "median_us": float(np.median(ts))}
+# the bench batch as two halves launched on two streams (two hardware queues: is the workgroup
+# dispatch of the one-wave blocks a limit?)
+th_d, ci_d, ac_d = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (theta, cid, active))
+out = torch.empty(len(cid), dtype=torch.float64, device=dev)
+h = len(cid) // 2
+s2 = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+
+
+def two():
+    ev = torch.cuda.Event()
+    ev.record(st)
+    for k, (a, b) in enumerate(((0, h), (h, len(cid)))):
+        s2[k].wait_event(ev)
+        lk.ss_batch_device(th_d[a:b], ci_d[a:b], out[a:b], ac_d[a:b], stream=s2[k])
+    for k in range(2):
+        e = torch.cuda.Event()
+        e.record(s2[k])
+        st.wait_event(e)
+
+
+for _ in range(10):
+    two()
+torch.cuda.synchronize()
+ts = []
+for _ in range(15):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(40):
+        two()
+    e1.record(st)
+    torch.cuda.synchronize()
+    ts.append(e0.elapsed_time(e1) / 40 * 1e3)
+res["bench_two_streams"] = {"rows": len(cid), "active": int(active.sum()), "median_us": float(np.median(ts))}
 print(json.dumps(res, indent=1))
