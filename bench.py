@@ -344,19 +344,26 @@ def synthetic_kernel(cfg: int, rank: int, world: int, device_index: int, proposa
 
 
 def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_steps: int, reduce,
-                         engine: str = "auto", n_points: int = 200, coll_device: str = None):
+                         engine: str = "auto", n_points: int = 200, coll_device: str = None,
+                         shard_cells: int = CONFIG_SHARD_CELLS, n_shards: int = CONFIG_SHARDS):
     """SURVEY.md §8(d) configs 4/5 end to end, as `parallel.fit_sharded` runs a sharded fit: 10,000
     synthetic cells in 8 fixed shards, rank r fits its shards (one GPU-resident DRAM chain per cell,
     n_burn = n_steps/20, chains keyed by the dataset-wide cell index, so the fit is the same at every
     GPU count), then ONE all-gather of the packed per-cell results (RCCL over xGMI on a multi-GPU node)
     -- inside the timed region, and timed on its own too. Strong scaling: 10,000 cells in total.
-    BASELINE configs 4/5 name n_steps = 200000 (the default); a smaller n_steps is labelled a sample."""
+    BASELINE configs 4/5 name n_steps = 200000 (the default); a smaller n_steps is labelled a sample.
+    With more ranks than shards a rank holds no cells: it builds no context and fits nothing, but joins
+    every collective (fit_sharded with lk=None)."""
+    import contextlib
+
     from transcriptioncycleinference_amd import Likelihood
     from transcriptioncycleinference_amd.mcmc import DramOptions
     from transcriptioncycleinference_amd.parallel import fit_sharded
 
-    cells, _, construct, n_total, n_points, lo, hi = synthetic_config_cells(cfg, rank, world, device_index, n_points)
-    with Likelihood(cells, construct, device=device_index) as lk:
+    cells, _, construct, n_total, n_points, lo, hi = synthetic_config_cells(cfg, rank, world, device_index, n_points,
+                                                                            shard_cells=shard_cells,
+                                                                            n_shards=n_shards)
+    with (Likelihood(cells, construct, device=device_index) if cells.n_cells else contextlib.nullcontext()) as lk:
         reduce(0.0, "max")  # barrier
         t0 = time.perf_counter()
         fr = fit_sharded(lk, device=coll_device, cell_offset=lo, n_steps=n_steps, n_burn=max(1, n_steps // 20),
@@ -379,11 +386,13 @@ def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_s
             s_cid = (loc.cell_index[sample] - lo).astype(np.int32)
             s_ss = lk.ss_batch(s_theta, s_cid)
             ok = ok and bool(np.all(np.isfinite(s_ss)))
+        else:
+            ok = ok and cells.n_cells == 0   # only a rank without cells has no local fit
     dev_s = fr.elapsed_ms * 1e-3     # max over ranks (fit_sharded)
     evals = int(fr.n_evals)          # summed over ranks (fit_sharded)
     gather_s = reduce(fr.gather_s, "max")
     acc = float(np.median([r for r in fr.accept_rate])) if len(fr.accept_rate) else float("nan")
-    out = {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points in {CONFIG_SHARDS} shards "
+    out = {"workload": f"config{cfg}: synthetic {n_total} cells x {n_points} points in {n_shards} shards "
                        f"(seed 20201028 + shard), construct {construct.name}, {hi - lo} chains on rank 0, "
                        f"{n_steps} steps, results all-gathered" + ("" if n_steps >= 200000 else
                                                                     " (bounded sample of the configured 200k)"),
@@ -408,9 +417,11 @@ def cpu_baseline_synth(cfg: int, spot: dict, seconds: float):
     outputs: the GPU SS of the same rows (synthetic_end_to_end) against the oracle's."""
     from oracle import c_oracle  # cpu_baseline leg only
 
-    c_oracle.build()
     cells, cs = spot["cells"], spot["construct"]
     th, ci = spot["theta"], spot["cid"]
+    if len(ci) == 0:  # rank 0 holds no shard (more ranks than shards)
+        return {"value": None, "unit": "SS evals/s", "kind": "port", "sample": "none: rank 0 fitted no cells"}
+    c_oracle.build()
     ac = np.ones(len(ci), np.uint8)
     threads = c_oracle.max_threads()
     want, st = c_oracle.ss_batch(cells.offsets, cells.t, cells.ms2, cells.pp7, cs, th, ci)
@@ -784,17 +795,33 @@ def main():
                 res[f"config{cfg}_dram"], spots[cfg] = synthetic_end_to_end(cfg, rank, world, device_index,
                                                                             args.synth_dram_steps, reduce,
                                                                             coll_device=str(coll_dev))
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(cells, theta_h, rounds_cid(cells, args.proposals), act_h, args.cpu_seconds)
-        res["cpu_fit_config1"] = cpu_fit_config1(lk)
-        for cfg, spot in spots.items():
-            res[f"cpu_baseline_config{cfg}"] = cpu_baseline_synth(cfg, spot, args.cpu_seconds / 2)
+    if distributed:
+        dist.barrier()   # every GPU leg of every rank is done before the host cores are timed
+    cpu_legs(res, rank, world, args, cells, theta_h, act_h, lk, spots)
     if rank == 0:
         print(json.dumps(res), flush=True)
     lk.close()
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def cpu_legs(res: dict, rank: int, world: int, args, cells, theta_h, act_h, lk, spots: dict):
+    """The CPU baselines beside the GPU numbers (BASELINE.md CPU plan), at EVERY world
+    size: on rank 0 only, after the last GPU leg of every rank (the caller's barrier), on the host
+    cores of the GPU box; the other ranks wait in the final barrier. With N ranks on one node the N
+    processes share those cores, which the `host` entry states."""
+    if rank != 0 or args.no_cpu_baseline:
+        return
+    host = {"os_cpu_count": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "ranks_on_this_host": world,
+            "note": "rank 0 times the CPU path after every rank's GPU legs; the other ranks idle in a barrier"
+            if world > 1 else "one rank"}
+    res["cpu_baseline"] = cpu_baseline(cells, theta_h, rounds_cid(cells, args.proposals), act_h, args.cpu_seconds)
+    res["cpu_baseline"]["host"] = host
+    res["cpu_fit_config1"] = cpu_fit_config1(lk)
+    for cfg, spot in spots.items():
+        res[f"cpu_baseline_config{cfg}"] = cpu_baseline_synth(cfg, spot, args.cpu_seconds / 2)
 
 
 def rounds_cid(cells, K: int) -> np.ndarray:

@@ -159,6 +159,10 @@ typedef struct {
   const int64_t* chain_keys; /* optional [n_chains]: chain c draws from RNG stream chain_keys[c]
                                 (NULL: stream c). Keying chains by their global cell index makes a
                                 shard of a run (its cells on one GPU) reproduce the unsharded chains */
+  int64_t adapt_pmax;   /* 0, or the largest P = 7 + N over every chain of a larger fit that this run is one
+                           shard of: the covariance adaptation kernel is picked by the largest P
+                           (k_adapt_gt past 208), so a shard passing the whole fit's value adapts with the
+                           same kernel, hence the same bits, as the unsharded fit (parallel.fit_sharded) */
 } tci_dram_options;
 
 /* DRAM engines; all give identical chains for the same seed.

@@ -47,9 +47,10 @@ typedef enum { mxREAL = 0, mxCOMPLEX = 1 } mxComplexity;
 
 typedef struct mxArray_tag mxArray;
 
-/* queries */
+/* queries (mxGetN of an N-D array is the product of its dimensions past the first, as in MATLAB) */
 mwSize mxGetNumberOfElements(const mxArray* a);
 mwSize mxGetNumberOfDimensions(const mxArray* a);
+const mwSize* mxGetDimensions(const mxArray* a);
 size_t mxGetM(const mxArray* a);
 size_t mxGetN(const mxArray* a);
 bool mxIsDouble(const mxArray* a);
@@ -66,6 +67,8 @@ void* mxGetData(const mxArray* a);
 double* mxGetPr(const mxArray* a);
 mxLogical* mxGetLogicals(const mxArray* a);
 mxArray* mxGetField(const mxArray* s, mwIndex i, const char* name);
+int mxGetNumberOfFields(const mxArray* s);
+const char* mxGetFieldNameByNumber(const mxArray* s, int n);
 char* mxArrayToString(const mxArray* a);
 void mxFree(void* p);
 
@@ -73,6 +76,7 @@ void mxFree(void* p);
 mxArray* mxCreateDoubleMatrix(size_t m, size_t n, mxComplexity c);
 mxArray* mxCreateDoubleScalar(double v);
 mxArray* mxCreateNumericMatrix(size_t m, size_t n, mxClassID cls, mxComplexity c);
+mxArray* mxCreateNumericArray(mwSize ndim, const mwSize* dims, mxClassID cls, mxComplexity c);
 mxArray* mxCreateLogicalMatrix(size_t m, size_t n);
 mxArray* mxCreateString(const char* s);
 mxArray* mxCreateStructMatrix(size_t m, size_t n, int nfields, const char** names);

@@ -14,7 +14,8 @@
 
 struct mxArray_tag {
   mxClassID cls = mxUNKNOWN_CLASS;
-  size_t m = 0, n = 0;
+  size_t m = 0, n = 0;                // rows, and the product of the dimensions past the first
+  std::vector<size_t> dims;           // every dimension (at least two)
   bool complex = false;
   std::vector<unsigned char> data;    // numeric / logical / char payload, column-major
   std::vector<std::string> fields;    // struct field names
@@ -38,6 +39,7 @@ mxArray* make(mxClassID c, size_t m, size_t n) {
   a->cls = c;
   a->m = m;
   a->n = n;
+  a->dims = {m, n};
   a->data.assign(m * n * elem_size(c), 0);
   return a;
 }
@@ -55,7 +57,8 @@ std::vector<void (*)(void)> g_at_exit;
 extern "C" {
 
 mwSize mxGetNumberOfElements(const mxArray* a) { return a->m * a->n; }
-mwSize mxGetNumberOfDimensions(const mxArray*) { return 2; }
+mwSize mxGetNumberOfDimensions(const mxArray* a) { return a->dims.size(); }
+const mwSize* mxGetDimensions(const mxArray* a) { return a->dims.data(); }
 size_t mxGetM(const mxArray* a) { return a->m; }
 size_t mxGetN(const mxArray* a) { return a->n; }
 bool mxIsDouble(const mxArray* a) { return a->cls == mxDOUBLE_CLASS; }
@@ -78,6 +81,11 @@ mxArray* mxGetField(const mxArray* s, mwIndex i, const char* name) {
   return nullptr;
 }
 
+int mxGetNumberOfFields(const mxArray* s) { return s->cls == mxSTRUCT_CLASS ? (int)s->fields.size() : 0; }
+const char* mxGetFieldNameByNumber(const mxArray* s, int n) {
+  return s->cls == mxSTRUCT_CLASS && n >= 0 && n < (int)s->fields.size() ? s->fields[n].c_str() : nullptr;
+}
+
 char* mxArrayToString(const mxArray* a) {
   if (a->cls != mxCHAR_CLASS) return nullptr;
   char* s = (char*)malloc(a->data.size() + 1);
@@ -94,6 +102,17 @@ mxArray* mxCreateDoubleScalar(double v) {
   return a;
 }
 mxArray* mxCreateNumericMatrix(size_t m, size_t n, mxClassID cls, mxComplexity) { return make(cls, m, n); }
+mxArray* mxCreateNumericArray(mwSize ndim, const mwSize* dims, mxClassID cls, mxComplexity) {
+  // trailing singleton dimensions are dropped down to two, as MATLAB does
+  std::vector<size_t> d(dims, dims + ndim);
+  while (d.size() > 2 && d.back() == 1) d.pop_back();
+  while (d.size() < 2) d.push_back(d.empty() ? 0 : 1);
+  size_t rest = 1;
+  for (size_t k = 1; k < d.size(); ++k) rest *= d[k];
+  mxArray* a = make(cls, d[0], rest);
+  a->dims = d;
+  return a;
+}
 mxArray* mxCreateLogicalMatrix(size_t m, size_t n) { return make(mxLOGICAL_CLASS, m, n); }
 mxArray* mxCreateString(const char* s) {
   const size_t k = strlen(s);

@@ -21,6 +21,21 @@
 //   [ms2, pp7] = tci_mex('forward', h, cell, x, 'raw' | 'interp')
 //   tci_mex('destroy', h)
 //   n = tci_mex('device_count')                 HIP devices visible to this MATLAB process
+//   [results, chain, s2chain, R] = tci_mex('dram', h, cells, X0, LB, UB, MU, SIG, J0, sigma2[, options])
+//          mcmcrun (TranscriptionCycleMCMC.m:273) for every chain at once on the GPU (tci_dram_run):
+//          one chain per COLUMN. cells: 1 x n; X0 / LB / UB (params, :242-255), MU / SIG (Gaussian
+//          priors, SIG = Inf: none, :254) and J0 (the diagonal of options.qcov, :230) are P x n with
+//          P >= 7 + N of every chain's cell (rows past a chain's 7 + N are ignored); sigma2: model.sigma2
+//          (:259), a scalar or 1 x n. options: mcmcstat's names -- nsimu, burnintime, adaptint, method
+//          ('dram' | 'am' | 'dr' | 'mh'), updatesigma, drscale, adascale, qcovadj, burnin_scale -- plus
+//          stats_from (first row of the summaries; default burnintime, the reference's n_burn, :276),
+//          thin (chain rows kept: 1, 1+thin, ...; default 1 when chain or s2chain is asked for), seed,
+//          engine ('auto' | 'fused' | 'walk' | 'batched'), max_chunk, chain_keys (1 x n RNG stream keys)
+//          and adapt_pmax; verbosity / waitbar / printint are accepted and ignored.
+//          results: struct with mean, std (std(...,1)), final_theta (P x n), sigma_mean, sigma_std
+//          (:302-303), accept_rate, n_evals (1 x n) and elapsed_ms; chain: P x n x ceil(nsimu/thin);
+//          s2chain: n x ceil(nsimu/thin); R: P x P x n upper factors with R(:,:,k)'*R(:,:,k) the final
+//          proposal covariance of chain k (mcmcstat results.qcov).
 // Errors are raised with mexErrMsgIdAndTxt('tci:...'), carrying tci_last_error().
 // Every argument's class and size is checked before a pointer reaches the C ABI. Live contexts
 // are tracked; a handle that this MEX file did not create (or already destroyed) is rejected,
@@ -28,6 +43,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <set>
 #include <string>
 #include <vector>
@@ -201,6 +217,191 @@ void cmd_forward(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   if (nlhs > 1) plhs[1] = pp7; else mxDestroyArray(pp7);
 }
 
+// ---- 'dram': the GPU-resident sampler -------------------------------------------------------
+
+double opt_num(const mxArray* o, const char* name, double def) {
+  const mxArray* f = o ? mxGetField(o, 0, name) : nullptr;
+  if (!f) return def;
+  if (!mxIsDouble(f) && !mxIsLogical(f)) mexErrMsgIdAndTxt("tci:opts", "options.%s must be numeric", name);
+  if (mxGetNumberOfElements(f) != 1) mexErrMsgIdAndTxt("tci:opts", "options.%s must be a scalar", name);
+  return mxIsLogical(f) ? (mxGetLogicals(f)[0] ? 1.0 : 0.0) : mxGetPr(f)[0];
+}
+
+int64_t opt_int(const mxArray* o, const char* name, int64_t def, int64_t lo) {
+  const double v = opt_num(o, name, (double)def);
+  if (!(v >= (double)lo && v <= 9.0e15) || v != (double)(int64_t)v)
+    mexErrMsgIdAndTxt("tci:opts", "options.%s must be an integer >= %lld", name, (long long)lo);
+  return (int64_t)v;
+}
+
+std::string opt_str(const mxArray* o, const char* name, const char* def) {
+  const mxArray* f = o ? mxGetField(o, 0, name) : nullptr;
+  if (!f) return def;
+  if (!mxIsChar(f)) mexErrMsgIdAndTxt("tci:opts", "options.%s must be a character vector", name);
+  std::string r = str_of(f);
+  for (char& ch : r) ch = (char)((ch >= 'A' && ch <= 'Z') ? ch - 'A' + 'a' : ch);
+  return r;
+}
+
+// A P x n real double matrix (one chain per column).
+const double* chain_matrix(const mxArray* a, const char* what, size_t P, size_t n) {
+  if (!mxIsDouble(a) || mxIsComplex(a) || mxIsSparse(a)) mexErrMsgIdAndTxt("tci:arg", "%s must be real double", what);
+  if (mxGetNumberOfDimensions(a) != 2 || mxGetM(a) != P || mxGetN(a) != n)
+    mexErrMsgIdAndTxt("tci:arg", "%s must be %d x %d (one chain per column, as X0)", what, (int)P, (int)n);
+  return mxGetPr(a);
+}
+
+void cmd_dram(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+  if (nrhs < 10 || nrhs > 11)
+    mexErrMsgIdAndTxt("tci:arg", "tci_mex('dram', h, cells, X0, LB, UB, MU, SIG, J0, sigma2[, options])");
+  // every argument and option is checked before the handle (and before anything reaches the GPU)
+  const size_t n = mxGetNumberOfElements(prhs[2]);
+  const double* c = doubles(prhs[2], -1, "cells");
+  if (n == 0) mexErrMsgIdAndTxt("tci:arg", "cells must name at least one chain's cell");
+  if (!mxIsDouble(prhs[3]) || mxGetNumberOfDimensions(prhs[3]) != 2 || mxGetN(prhs[3]) != n)
+    mexErrMsgIdAndTxt("tci:arg", "X0 must be P x n: one chain per column, n = numel(cells)");
+  const size_t P = mxGetM(prhs[3]);
+  if (P < 7) mexErrMsgIdAndTxt("tci:arg", "X0 must have at least 7 rows ([v, tau, ton, MS2_basal, PP7_basal, A, R, dR])");
+  const char* names[6] = {"X0", "LB", "UB", "MU", "SIG", "J0"};
+  const double* in[6];
+  for (int k = 0; k < 6; ++k) in[k] = chain_matrix(prhs[3 + k], names[k], P, n);
+  const size_t ns2 = mxGetNumberOfElements(prhs[9]);
+  const double* s2 = doubles(prhs[9], -1, "sigma2");
+  if (ns2 != 1 && ns2 != n) mexErrMsgIdAndTxt("tci:arg", "sigma2 must be a scalar or have one entry per chain");
+  std::vector<int32_t> cid(n);
+  for (size_t b = 0; b < n; ++b) {
+    if (!(c[b] >= 1 && c[b] <= 2147483647.0) || c[b] != (double)(int64_t)c[b])
+      mexErrMsgIdAndTxt("tci:arg", "cells(%d) must be a positive integer", (int)b + 1);
+    cid[b] = (int32_t)c[b] - 1;
+  }
+  std::vector<double> s2v(n);
+  for (size_t b = 0; b < n; ++b) s2v[b] = s2[ns2 == 1 ? 0 : b];
+
+  // options: mcmcstat's names (TranscriptionCycleMCMC.m:263-270), unknown fields refused
+  const mxArray* o = nullptr;
+  if (nrhs > 10 && !(mxIsDouble(prhs[10]) && mxGetNumberOfElements(prhs[10]) == 0)) {  // [] = defaults
+    if (!mxIsStruct(prhs[10]) || mxGetNumberOfElements(prhs[10]) != 1)
+      mexErrMsgIdAndTxt("tci:opts", "options must be a 1x1 struct");
+    o = prhs[10];
+    static const char* known[] = {"nsimu", "burnintime", "adaptint", "method", "updatesigma", "drscale", "adascale",
+                                  "qcovadj", "burnin_scale", "stats_from", "thin", "seed", "engine", "max_chunk",
+                                  "chain_keys", "adapt_pmax", "verbosity", "waitbar", "printint"};
+    for (int f = 0; f < mxGetNumberOfFields(o); ++f) {
+      const char* fn = mxGetFieldNameByNumber(o, f);
+      bool ok = false;
+      for (const char* k : known) ok = ok || strcmp(fn, k) == 0;
+      if (!ok && strcmp(fn, "qcov") == 0)
+        mexErrMsgIdAndTxt("tci:opts", "options.qcov: pass the initial proposal variances as J0 (P x n)");
+      if (!ok) mexErrMsgIdAndTxt("tci:opts", "options.%s is not an option of tci_mex('dram')", fn);
+    }
+  }
+  tci_dram_options opt;
+  tci_dram_defaults(&opt);
+  opt.n_steps = opt_int(o, "nsimu", opt.n_steps, 1);
+  opt.burnintime = opt_int(o, "burnintime", opt.burnintime, 0);
+  opt.adaptint = opt_int(o, "adaptint", opt.adaptint, 0);
+  const std::string method = opt_str(o, "method", "dram");  // mcmcstat: mh, am, dr, dram
+  if (method == "dram" || method == "am") {
+    opt.ntry = method == "dram" ? 2 : 1;
+  } else if (method == "dr" || method == "mh") {
+    opt.ntry = method == "dr" ? 2 : 1;
+    opt.adaptint = 0;
+  } else {
+    mexErrMsgIdAndTxt("tci:opts", "options.method must be 'dram', 'am', 'dr' or 'mh'");
+  }
+  opt.updatesigma = opt_num(o, "updatesigma", opt.updatesigma) != 0.0 ? 1 : 0;
+  opt.drscale = opt_num(o, "drscale", opt.drscale);
+  opt.adascale = opt_num(o, "adascale", opt.adascale);
+  opt.qcovadj = opt_num(o, "qcovadj", opt.qcovadj);
+  opt.burnin_scale = opt_num(o, "burnin_scale", opt.burnin_scale);
+  opt.stats_from = opt_int(o, "stats_from", std::max<int64_t>(opt.burnintime, 1), 1);
+  const bool want_chain = nlhs >= 2;
+  const int64_t thin = opt_int(o, "thin", 1, 0);
+  opt.thin = want_chain ? thin : 0;
+  opt.seed = (uint64_t)opt_int(o, "seed", (int64_t)opt.seed, 0);
+  const std::string engine = opt_str(o, "engine", "auto");
+  if (engine == "auto") opt.engine = TCI_DRAM_AUTO;
+  else if (engine == "fused") opt.engine = TCI_DRAM_FUSED;
+  else if (engine == "batched") opt.engine = TCI_DRAM_BATCHED;
+  else if (engine == "walk") opt.engine = TCI_DRAM_WALK;
+  else mexErrMsgIdAndTxt("tci:opts", "options.engine must be 'auto', 'fused', 'walk' or 'batched'");
+  opt.max_chunk = (int32_t)opt_int(o, "max_chunk", 0, 0);
+  opt.adapt_pmax = opt_int(o, "adapt_pmax", 0, 0);
+  std::vector<int64_t> keys;
+  if (const mxArray* k = o ? mxGetField(o, 0, "chain_keys") : nullptr) {
+    const double* kv = doubles(k, (long long)n, "options.chain_keys");
+    keys.resize(n);
+    for (size_t b = 0; b < n; ++b) {
+      if (!(kv[b] >= 0 && kv[b] <= 9.0e15) || kv[b] != (double)(int64_t)kv[b])
+        mexErrMsgIdAndTxt("tci:opts", "options.chain_keys(%d) must be a non-negative integer", (int)b + 1);
+      keys[b] = (int64_t)kv[b];
+    }
+    opt.chain_keys = keys.data();
+  }
+
+  tci_ctx* ctx = handle_of(prhs[1]);
+  // outputs, written in place: the ABI's row-major [chain][P] is MATLAB's column-major P x n
+  static const char* fields[] = {"mean", "std", "final_theta", "sigma_mean", "sigma_std", "accept_rate", "n_evals",
+                                 "elapsed_ms"};
+  mxArray* res = mxCreateStructMatrix(1, 1, 8, fields);
+  mxArray* pn[6];
+  for (int k = 0; k < 3; ++k) pn[k] = mxCreateDoubleMatrix(P, n, mxREAL);
+  for (int k = 3; k < 6; ++k) pn[k] = mxCreateDoubleMatrix(1, n, mxREAL);
+  for (int k = 0; k < 6; ++k) mxSetField(res, 0, fields[k], pn[k]);
+  std::vector<int64_t> nev(n);
+  tci_dram_outputs out;
+  memset(&out, 0, sizeof out);
+  out.mean = mxGetPr(pn[0]);
+  out.std = mxGetPr(pn[1]);
+  out.final_theta = mxGetPr(pn[2]);
+  out.sigma_mean = mxGetPr(pn[3]);
+  out.sigma_std = mxGetPr(pn[4]);
+  out.accept_rate = mxGetPr(pn[5]);
+  out.n_evals = nev.data();
+  const size_t n_keep = opt.thin > 0 ? (size_t)((opt.n_steps + opt.thin - 1) / opt.thin) : 0;
+  mxArray* ch = nullptr;
+  mxArray* s2c = nullptr;
+  if (want_chain) {
+    const mwSize d3[3] = {P, n, n_keep};
+    ch = mxCreateNumericArray(3, d3, mxDOUBLE_CLASS, mxREAL);  // P x n x n_keep == [row][chain][P]
+    s2c = mxCreateDoubleMatrix(n, n_keep, mxREAL);            // n x n_keep == [row][chain]
+    if (n_keep) {
+      out.chain = mxGetPr(ch);
+      out.s2chain = mxGetPr(s2c);
+    }
+  }
+  std::vector<double> rbuf;
+  if (nlhs >= 4) {
+    rbuf.resize(n * P * P);
+    out.qcov_R = rbuf.data();
+  }
+  const int rc = tci_dram_run(ctx, &opt, (int64_t)n, cid.data(), in[0], in[1], in[2], in[3], in[4], in[5], s2v.data(),
+                              (int64_t)P, &out);
+  if (rc != TCI_OK) {
+    mxDestroyArray(res);
+    if (ch) mxDestroyArray(ch);
+    if (s2c) mxDestroyArray(s2c);
+    check(ctx, rc, "tci_dram_run");
+  }
+  mxArray* ne = mxCreateDoubleMatrix(1, n, mxREAL);
+  for (size_t b = 0; b < n; ++b) mxGetPr(ne)[b] = (double)nev[b];
+  mxSetField(res, 0, "n_evals", ne);
+  mxSetField(res, 0, "elapsed_ms", mxCreateDoubleScalar(out.elapsed_ms));
+  plhs[0] = res;
+  if (nlhs >= 2) plhs[1] = ch;
+  if (nlhs >= 3) plhs[2] = s2c;
+  else if (s2c) mxDestroyArray(s2c);
+  if (nlhs >= 4) {  // [chain][i][j] (upper) -> R(i, j, chain): MATLAB's column-major
+    const mwSize d3[3] = {P, P, n};
+    mxArray* R = mxCreateNumericArray(3, d3, mxDOUBLE_CLASS, mxREAL);
+    double* r = mxGetPr(R);
+    for (size_t k = 0; k < n; ++k)
+      for (size_t i = 0; i < P; ++i)
+        for (size_t j = 0; j < P; ++j) r[k * P * P + j * P + i] = rbuf[k * P * P + i * P + j];
+    plhs[3] = R;
+  }
+}
+
 }  // namespace
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
@@ -215,6 +416,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   else if (cmd == "ss") cmd_ss(plhs, nrhs, prhs);
   else if (cmd == "ss_batch") cmd_ss_batch(plhs, nrhs, prhs);
   else if (cmd == "forward") cmd_forward(nlhs, plhs, nrhs, prhs);
+  else if (cmd == "dram") cmd_dram(nlhs, plhs, nrhs, prhs);
   else if (cmd == "device_count") {
     int n = 0;
     tci_device_count(&n);

@@ -34,6 +34,11 @@ class Mex:
             "mxGetM": (C.c_size_t, [_vp]),
             "mxGetN": (C.c_size_t, [_vp]),
             "mxGetClassID": (C.c_int, [_vp]),
+            "mxGetNumberOfDimensions": (C.c_size_t, [_vp]),
+            "mxGetDimensions": (C.POINTER(C.c_size_t), [_vp]),
+            "mxGetNumberOfFields": (C.c_int, [_vp]),
+            "mxGetFieldNameByNumber": (C.c_char_p, [_vp, C.c_int]),
+            "mxGetField": (_vp, [_vp, C.c_size_t, C.c_char_p]),
             "mexstub_call": (C.c_int, [C.c_int, C.POINTER(_vp), C.c_int, C.POINTER(_vp)]),
             "mexstub_error_id": (C.c_char_p, []),
             "mexstub_error_msg": (C.c_char_p, []),
@@ -56,14 +61,16 @@ class Mex:
         m, n = a.shape
         p = self.L.mxCreateDoubleMatrix(m, n, 0)
         if m * n:
-            C.memmove(self.L.mxGetData(p), np.asfortranarray(a).ctypes.data, 8 * m * n)
+            f = np.asfortranarray(a)   # held until the copy is done (a temporary's buffer would be freed)
+            C.memmove(self.L.mxGetData(p), f.ctypes.data, 8 * m * n)
         return p
 
     def logical(self, a) -> int:
         a = np.asarray(a, bool).reshape(1, -1)
         p = self.L.mxCreateLogicalMatrix(1, a.shape[1])
         if a.size:
-            C.memmove(self.L.mxGetData(p), a.astype(np.uint8).ctypes.data, a.size)
+            u8 = a.astype(np.uint8)
+            C.memmove(self.L.mxGetData(p), u8.ctypes.data, a.size)
         return p
 
     def string(self, s: str) -> int:
@@ -72,26 +79,40 @@ class Mex:
     def handle(self, v: int) -> int:
         return self.L.mexstub_make_uint64(v)
 
+    def value(self, v) -> int:
+        """str -> char, bool -> logical scalar, anything else -> double."""
+        if isinstance(v, str):
+            return self.string(v)
+        if isinstance(v, (bool, np.bool_)):
+            return self.logical([bool(v)])
+        return self.double(v)
+
     def struct(self, rows, fields) -> int:
-        """A 1 x len(rows) struct array; rows: list of dicts field -> value (numpy or str)."""
+        """A 1 x len(rows) struct array; rows: list of dicts field -> value (numpy, str or bool)."""
         names = (C.c_char_p * len(fields))(*[f.encode() for f in fields])
         p = self.L.mxCreateStructMatrix(1, len(rows), len(fields), names)
         for i, r in enumerate(rows):
             for f in fields:
                 if f in r:
                     v = r[f]
-                    self.L.mxSetField(p, i, f.encode(), self.string(v) if isinstance(v, str) else self.double(v))
+                    self.L.mxSetField(p, i, f.encode(), self.value(v))
         return p
 
-    def to_numpy(self, p) -> np.ndarray:
+    def to_numpy(self, p):
+        """A double / uint64 array as numpy (its MATLAB shape, N-D included), a 1x1 struct as a dict."""
         m, n = self.L.mxGetM(p), self.L.mxGetN(p)
         cls = self.L.mxGetClassID(p)
         if cls == 15:  # mxUINT64_CLASS
             return np.array([[self.L.mexstub_uint64(p)]], np.uint64)
-        out = np.empty((n, m), np.float64)
+        if cls == 2:  # mxSTRUCT_CLASS: field -> value of element 1
+            names = [self.L.mxGetFieldNameByNumber(p, f).decode() for f in range(self.L.mxGetNumberOfFields(p))]
+            return {f: self.to_numpy(self.L.mxGetField(p, 0, f.encode())) for f in names}
+        nd = self.L.mxGetNumberOfDimensions(p)
+        dims = tuple(self.L.mxGetDimensions(p)[k] for k in range(nd))
+        out = np.empty(m * n, np.float64)
         if m * n:
             C.memmove(out.ctypes.data, self.L.mxGetData(p), 8 * m * n)
-        return out.T  # column-major -> (m, n)
+        return out.reshape(dims, order="F")  # column-major -> MATLAB's shape
 
     # -- calls --------------------------------------------------------------------------------
     def call(self, *args, nlhs: int = 1):

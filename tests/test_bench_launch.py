@@ -87,3 +87,31 @@ def test_no_gpu_refused_for_one_rank():
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 2
     assert "needs 1 visible GPU(s), found 0" in r.stderr
+
+
+@pytest.mark.parametrize("rank,world", [(0, 1), (0, 2), (0, 8), (1, 2), (3, 8)])
+def test_cpu_baseline_is_in_the_line_at_every_world_size(monkeypatch, rank, world):
+    """the CPU baseline legs run on rank 0 at any world size (not only N = 1), so
+    every line of a 1/2/4/8-GPU scaling run carries `cpu_baseline` next to the GPU numbers; other
+    ranks skip them. The legs themselves are stubbed here (the real ones are exercised on the GPU box)."""
+    from types import SimpleNamespace
+
+    monkeypatch.setattr(bench, "cpu_baseline", lambda *a, **k: {"value": 1.0, "unit": "SS evals/s"})
+    monkeypatch.setattr(bench, "cpu_fit_config1", lambda *a, **k: {"value": 2.0})
+    monkeypatch.setattr(bench, "cpu_baseline_synth", lambda cfg, *a, **k: {"value": float(cfg)})
+
+    class C:
+        n_cells = 3
+
+    res = {}
+    bench.cpu_legs(res, rank, world, SimpleNamespace(no_cpu_baseline=False, proposals=4, cpu_seconds=1.0), C(),
+                   None, None, None, {4: {}, 5: {}})
+    if rank == 0:
+        assert set(res) == {"cpu_baseline", "cpu_fit_config1", "cpu_baseline_config4", "cpu_baseline_config5"}
+        assert res["cpu_baseline"]["host"]["ranks_on_this_host"] == world
+    else:
+        assert res == {}
+    res = {}
+    bench.cpu_legs(res, rank, world, SimpleNamespace(no_cpu_baseline=True, proposals=4, cpu_seconds=1.0), C(),
+                   None, None, None, {})
+    assert res == {}

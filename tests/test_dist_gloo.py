@@ -161,3 +161,79 @@ def test_unpack_results_of_a_shard_local_rank():
             np.testing.assert_array_equal(p["t_plot"], cells.cell(c)[0])
         else:
             assert len(p["t_plot"]) == 0
+
+
+class _StubLikelihood:
+    """What fit_sharded reads of a Likelihood (cells, construct.L0, info) -- no GPU context."""
+
+    def __init__(self, cells, rpl=2):
+        from types import SimpleNamespace
+
+        self.cells = cells
+        self.construct = SimpleNamespace(L0=6.626)
+        self.info = {"rows_per_lane": rpl}
+
+
+def _empty_rank_worker(rank, world, port, q, blocks):
+    """fit_sharded in the cell_offset layout with the GPU fit replaced by a deterministic stand-in;
+    ranks whose block is empty pass lk=None (more ranks than shards: bench.config_shards)."""
+    import torch.distributed as dist
+
+    import transcriptioncycleinference_amd.mcmc as M
+    from transcriptioncycleinference_amd import testdata
+    from transcriptioncycleinference_amd.parallel import fit_sharded, pack_results
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    full = testdata()
+    seen = {}
+
+    def fake_fit(lk, cells=None, cell_offset=0, opts=None, **kw):
+        seen["adapt_pmax"] = opts.adapt_pmax
+        return _fake_fit(full, [cell_offset + c for c in cells])
+
+    M.fit = fake_fit
+    lo, hi = blocks[rank]
+    lk = _StubLikelihood(full.subset(range(lo, hi))) if hi > lo else None
+    fr = fit_sharded(lk, cell_offset=lo)
+    q.put((rank, pack_results(fr, int(full.lengths.max())), seen.get("adapt_pmax"), fr.rows_per_lane_uniform,
+           fr.local is None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world3_fit_sharded_with_a_rank_without_cells():
+    """with more ranks than shards some ranks hold no cells. fit_sharded(lk=None) on such a
+    rank fits nothing but joins the all-reduce and the all-gather, so no rank waits forever; every rank
+    ends with the whole dataset's rows in cell order, and the ranks that fit pass the fit-wide largest
+    P (adapt_pmax) to the sampler. Rank 0 is the empty one here, as bench.config_shards gives it at
+    N > 8 (3 ranks, 2 shards: config_shards(0, 3, 2) is empty)."""
+    import bench
+    from transcriptioncycleinference_amd import testdata
+
+    full = testdata()
+    shards = [(0, 150), (150, 299)]
+    owned = [list(bench.config_shards(r, 3, 2)) for r in range(3)]
+    assert owned == [[], [0], [1]]
+    blocks = [(shards[o[0]][0], shards[o[-1]][1]) if o else (0, 0) for o in owned]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_empty_rank_worker, args=(r, 3, port, q, blocks)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = dict((r[0], r[1:]) for r in (q.get(timeout=240) for _ in range(3)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = _fake_fit(full, range(299))
+    from transcriptioncycleinference_amd.parallel import pack_results
+
+    rows = pack_results(want, int(full.lengths.max()))
+    pmax = 7 + int(full.lengths.max())
+    for r in range(3):
+        np.testing.assert_array_equal(got[r][0], rows)
+        assert got[r][1] == (None if r == 0 else pmax)
+        assert got[r][2] is True
+    assert got[0][3] and not got[1][3]

@@ -622,17 +622,19 @@ def test_very_long_cells_sample_and_adapt(n):
         np.testing.assert_allclose(R.T @ R, want, rtol=1e-10, atol=1e-10 * np.abs(want).max())  # FP64 R, P <= 520
 
 
-def test_walk_at_10000_chains_equals_fused_and_batched():
-    """BASELINE config 4 at its full chain count (10,000 synthetic cells x 200 points, one chain per
-    cell): WALK -- what AUTO runs there -- against FUSED and the batched engine, bit for bit, over
-    two adaptation windows (chunks cut by the draws-buffer cap, windows continuing across chunks);
-    every output finite."""
+@pytest.mark.parametrize("cfg", [4, 5])
+def test_walk_at_10000_chains_equals_fused_and_batched(cfg, c_oracle):
+    """BASELINE configs 4 and 5 at their full chain count (10,000 synthetic cells x 200 points, one chain
+    per cell; config 5 on the two-segment, 3x-length construct, whose WALK instance keeps its bounds in
+    registers): WALK -- what AUTO runs there -- against FUSED and the batched engine, bit for bit, over
+    two adaptation windows; every output finite, and the SS of 256 of the 10,000 final states equal to
+    the C oracle's (SumofSquares...m:28-64 restated) within 1e-10."""
     import bench
     from transcriptioncycleinference_amd import Likelihood
     from transcriptioncycleinference_amd.mcmc import DramOptions, fit
 
-    cells, _, construct = bench.synthetic_config_cells(4, 0, 1, 0)[:3]
-    assert cells.n_cells == 10000
+    cells, _, construct = bench.synthetic_config_cells(cfg, 0, 1, 0)[:3]
+    assert cells.n_cells == 10000 and construct.n_seg == (1 if cfg == 4 else 2)
     out = {}
     with Likelihood(cells, construct, device=0) as L:
         for eng in ("walk", "fused", "batched"):
@@ -648,6 +650,13 @@ def test_walk_at_10000_chains_equals_fused_and_batched():
         np.testing.assert_array_equal(o.n_evals, w.n_evals, err_msg=eng)
         np.testing.assert_array_equal([r["mean_v"] for r in o.MCMCresults], [r["mean_v"] for r in w.MCMCresults],
                                       err_msg=eng)
+    sample = np.linspace(0, 9999, 256).astype(np.int64)
+    th = np.ascontiguousarray(w.final_theta[sample])
+    with Likelihood(cells, construct, device=0) as L:
+        got = L.ss_batch(th, sample.astype(np.int32))
+    want, st = c_oracle.ss_batch(cells.offsets, cells.t, cells.ms2, cells.pp7, construct, th, sample.astype(np.int32))
+    assert np.all(st == 0)
+    np.testing.assert_allclose(got, want, rtol=1e-10, atol=0)
 
 
 @pytest.mark.parametrize("engine", ["fused", "walk", "batched"])
@@ -875,9 +884,12 @@ def test_config4_sharded_fit_is_the_same_at_every_world_size():
 
 
 def test_adaptint_past_the_adaptation_lds_is_refused_before_any_launch(c_oracle):
-    """ADVICE r04: the adaptation kernel's run table grows with adaptint (8 bytes per window row);
+    """ADVICE r04: the adaptation kernel's run table grows with adaptint (4 bytes per window row);
     an adaptint whose table no longer fits a CU's LDS is refused with TCI_ERANGE up front (nothing
-    launched), and one that fits runs."""
+    launched), and one that fits runs. ADVICE r05: the check counts the kernel's static LDS too -- at
+    config 4's P = 207 (k_adapt_mfma<8, 13, 12>) adaptint 26,815 fills the 160 KiB with dynamic LDS
+    alone ((13 * 512 + 2 * 208) * 8 + 4 * 26,816 bytes), so the kernel's own __shared__ words make it
+    one that cannot launch: refused; 26,751 leaves 256 bytes for them and runs."""
     from transcriptioncycleinference_amd import Likelihood, _lib
     from transcriptioncycleinference_amd.mcmc import DramOptions, dram_run
 
@@ -887,7 +899,102 @@ def test_adaptint_past_the_adaptation_lds_is_refused_before_any_launch(c_oracle)
         args = (np.array(plan.cells[:2], np.int32), plan.x0[sl], plan.lower[sl], plan.upper[sl], plan.prior_mu[sl],
                 plan.prior_sig[sl], plan.qcov_diag[sl], 1.0)
         with pytest.raises(_lib.TciError) as ei:
-            dram_run(L, *args, DramOptions(n_steps=50, burnintime=10, adaptint=20000, stats_from=1))
+            dram_run(L, *args, DramOptions(n_steps=50, burnintime=10, adaptint=40000, stats_from=1))
         assert ei.value.code == _lib.TCI_ERANGE and "LDS" in str(ei.value)
         ok = dram_run(L, *args, DramOptions(n_steps=3000, burnintime=10, adaptint=1500, stats_from=1))
         assert np.all(np.isfinite(ok.mean[:, :207]))
+        dyn = (13 * 512 + 2 * 208) * 8 + (26815 + 1) * 4
+        assert dyn == 160 * 1024
+        with pytest.raises(_lib.TciError) as ei:
+            dram_run(L, *args, DramOptions(n_steps=50, burnintime=10, adaptint=26815, stats_from=1))
+        assert ei.value.code == _lib.TCI_ERANGE and "LDS" in str(ei.value)
+        edge = dram_run(L, *args, DramOptions(n_steps=26760, burnintime=10, adaptint=26751, stats_from=1))
+        assert np.all(np.isfinite(edge.mean[:, :207])) and np.all(edge.n_evals > 0)
+
+
+def test_shard_without_long_cells_adapts_like_the_unsharded_fit():
+    """the adaptation kernel is picked by the largest P of a run (k_adapt_gt past 208), and the
+    two kernels scatter in different orders. A shard whose cells are all P = 207 passes the whole fit's
+    largest P (DramOptions.adapt_pmax, as parallel.fit_sharded all-reduces it) and then equals the
+    unsharded fit -- which holds two P = 217 cells -- bit for bit."""
+    from transcriptioncycleinference_amd import Likelihood, from_lists
+    from transcriptioncycleinference_amd.construct import builtin_construct
+    from transcriptioncycleinference_amd.data import synthetic_cells
+    from transcriptioncycleinference_amd.mcmc import DramOptions, fit
+
+    cs = builtin_construct("P2P-MS2v5-LacZ-PP7v4")
+
+    def fwd(times, theta):
+        nan = [np.full(len(t), np.nan) for t in times]
+        with Likelihood(from_lists([(t, a, a) for t, a in zip(times, nan)]), cs, device=0) as L:
+            return L.forward(theta, np.arange(len(times), dtype=np.int32), grid="interp")
+
+    a, _ = synthetic_cells(6, 200, 11, fwd)
+    b, _ = synthetic_cells(2, 210, 12, fwd)
+    full = from_lists([a.cell(k) for k in range(6)] + [b.cell(k) for k in range(2)])
+    kw = dict(n_steps=450, n_burn=150, seed=4)
+    with Likelihood(full, cs, device=0) as L:
+        assert L.info["rows_per_lane"] == 4
+        one = fit(L, **kw)
+    with Likelihood(full.subset(range(6)), cs, device=0) as L:
+        assert L.info["rows_per_lane"] == 4
+        shard = fit(L, opts=DramOptions(adapt_pmax=217), **kw)
+        own = fit(L, **kw)                                          # picks k_adapt_mfma for its own P = 207
+    np.testing.assert_array_equal(shard.final_theta[:, :207], one.final_theta[:6, :207])
+    for k in range(6):
+        for f in ("mean_v", "sigma_v", "mean_R", "mean_sigma", "mean_dR", "sigma_dR"):
+            np.testing.assert_array_equal(shard.MCMCresults[k][f], one.MCMCresults[k][f], err_msg=f)
+    assert np.all(np.isfinite(own.final_theta[:, :207]))
+
+
+def _empty_rank_bench_worker(rank, world, port, q):
+    """bench.synthetic_end_to_end with more ranks than shards (gloo, every rank on this GPU): rank 0
+    owns no shard, builds no context, and still joins every collective."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def reduce(x, op):
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        return float(t.item())
+
+    out, spot = bench.synthetic_end_to_end(4, rank, world, 0, 200, reduce, coll_device="cpu", shard_cells=16,
+                                           n_shards=2)
+    q.put((rank, out["chains"], out["outputs_finite"], out["ssfun_evals"], len(spot["cid"])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_config_end_to_end_with_more_ranks_than_shards():
+    """bench.py's config-4/5 DRAM leg at N > 8 gave some ranks no shard; such a
+    rank raised building a 0-cell context while the others waited in the collectives. Here 3 ranks over
+    2 shards of 16 cells: every rank finishes, and every rank reports the 32 gathered chains."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_empty_rank_bench_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = dict((r[0], r[1:]) for r in (q.get(timeout=300) for _ in range(3)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(3):
+        chains, finite, evals, n_spot = got[r]
+        assert chains == 32 and finite and evals == got[0][2]
+        assert n_spot == (0 if r == 0 else 16)

@@ -186,3 +186,140 @@ def test_custom_construct_struct_and_destroy(mex, cells):
     mex.call("destroy", hp, nlhs=0)
     expect("tci:handle", mex.call, "ss", hp, 1.0, rows[0])   # a destroyed handle is rejected
     hp.free()
+
+
+# ---- 'dram': the GPU-resident sampler through the gateway (TranscriptionCycleMCMC.m:161-273) ----
+
+
+def _dram_args(mex, cells, ids, seed=5):
+    """The reference's per-cell setup (mcmc.plan_fit, :193-255) as MATLAB holds it: P x n, one chain
+    per column, 1-based cells."""
+    from transcriptioncycleinference_amd.mcmc import plan_fit
+
+    plan = plan_fit(cells, ids, seed)
+    cols = [a.T.copy() for a in (plan.x0, plan.lower, plan.upper, plan.prior_mu, plan.prior_sig, plan.qcov_diag)]
+    return plan, [np.asarray(plan.cells, np.float64) + 1] + cols + [1.0]
+
+
+def _opts(mex, **kv):
+    return MxPtr(mex, mex.struct([kv], list(kv)))
+
+
+def test_dram_arguments_and_options_are_checked(mex, cells):
+    """Every argument and option of tci_mex('dram', ...) is checked before the handle is looked at
+    (so these run without a GPU); a well-formed call with a dead handle reaches the handle check."""
+    fake = MxPtr(mex, mex.handle(12345))
+    plan, a = _dram_args(mex, cells, [0, 1, 2])
+    P = a[1].shape[0]
+    expect("tci:handle", mex.call, "dram", fake, *a)                       # well-formed: only the handle is bad
+    expect("tci:arg", mex.call, "dram", fake, *a[:6])                      # too few arguments
+    expect("tci:arg", mex.call, "dram", fake, a[0][:2], *a[1:])            # n differs from X0's columns
+    expect("tci:arg", mex.call, "dram", fake, a[0] + 0.5, *a[1:])          # non-integer cells
+    expect("tci:arg", mex.call, "dram", fake, a[0] - a[0], *a[1:])         # cells are 1-based
+    expect("tci:arg", mex.call, "dram", fake, a[0], a[1][:6], *a[2:])      # fewer than 7 rows
+    for k in range(2, 7):                                                  # LB .. J0 must match X0's shape
+        bad = list(a)
+        bad[k] = a[k][:P - 1]
+        e = expect("tci:arg", mex.call, "dram", fake, *bad)
+        assert ("LB", "UB", "MU", "SIG", "J0")[k - 2] in e.msg
+    expect("tci:arg", mex.call, "dram", fake, *a[:-1], np.ones(2))         # sigma2: scalar or one per chain
+    expect("tci:handle", mex.call, "dram", fake, *a[:-1], np.ones(3))
+    expect("tci:handle", mex.call, "dram", fake, *a, np.zeros((0, 0)))     # [] = default options
+    expect("tci:opts", mex.call, "dram", fake, *a, 3.0)                    # options must be a struct
+    cases = [({"nsimu": 0.0}, "nsimu"), ({"nsimu": 10.5}, "nsimu"), ({"adaptint": -1.0}, "adaptint"),
+             ({"method": "slice"}, "method"), ({"method": 3.0}, "method"), ({"engine": "gpu"}, "engine"),
+             ({"qcov": np.eye(P)}, "J0"), ({"nsimul": 100.0}, "nsimul"), ({"thin": [1.0, 2.0]}, "thin"),
+             ({"chain_keys": [-1.0, 2.0, 3.0]}, "chain_keys")]
+    for kv, word in cases:
+        o = _opts(mex, **kv)
+        e = expect("tci:opts", mex.call, "dram", fake, *a, o)
+        assert word in e.msg, (kv, e.msg)
+        o.free()
+    o = _opts(mex, chain_keys=[1.0, 2.0])                                  # one key per chain
+    expect("tci:arg", mex.call, "dram", fake, *a, o)
+    o.free()
+    o = _opts(mex, nsimu=50.0, method="AM", verbosity=0.0, updatesigma=True, engine="walk")
+    expect("tci:handle", mex.call, "dram", fake, *a, o)                    # mcmcstat's names, case-insensitive
+    o.free()
+
+
+def _dram_gateway_vs_binding(mex, h, lk, cells, ids, opts_kv, nlhs=4):
+    from transcriptioncycleinference_amd.mcmc import DramOptions, dram_run
+
+    plan, a = _dram_args(mex, cells, ids)
+    keys = np.asarray(plan.cells, np.int64) * 3 + 11
+    o = _opts(mex, **opts_kv, chain_keys=keys.astype(np.float64))
+    res, ch, s2c, R = mex.call("dram", h, *a, o, nlhs=nlhs)
+    o.free()
+    do = DramOptions(n_steps=int(opts_kv["nsimu"]), burnintime=int(opts_kv["burnintime"]),
+                     adaptint=int(opts_kv.get("adaptint", 100)), stats_from=int(opts_kv["burnintime"]),
+                     thin=int(opts_kv.get("thin", 1)), seed=int(opts_kv["seed"]),
+                     engine=opts_kv.get("engine", "auto"))
+    want = dram_run(lk, np.asarray(plan.cells, np.int32), plan.x0, plan.lower, plan.upper, plan.prior_mu,
+                    plan.prior_sig, plan.qcov_diag, 1.0, do, want_qcov=True, chain_keys=keys)
+    n, P = plan.x0.shape
+    for f in ("mean", "std", "final_theta"):
+        assert res[f].shape == (P, n)
+        np.testing.assert_array_equal(res[f], getattr(want, f).T, err_msg=f)
+    for f in ("sigma_mean", "sigma_std", "accept_rate"):
+        np.testing.assert_array_equal(res[f][0], getattr(want, f), err_msg=f)
+    np.testing.assert_array_equal(res["n_evals"][0], want.n_evals.astype(np.float64))
+    assert ch.shape == (P, n, want.chain.shape[0]) and s2c.shape == (n, want.chain.shape[0])
+    np.testing.assert_array_equal(np.transpose(ch, (2, 1, 0)), want.chain)     # P x n x rows == [row][chain][P]
+    np.testing.assert_array_equal(s2c.T, want.s2chain)
+    assert R.shape == (P, P, n)
+    np.testing.assert_array_equal(np.transpose(R, (2, 0, 1)), want.qcov_R)     # R(:,:,k) upper, qcov = R'R
+    for k in range(n):
+        assert np.all(np.tril(R[:, :, k], -1) == 0)
+    return plan, res
+
+
+@pytest.mark.gpu
+def test_dram_equals_the_binding_bitwise_on_testdata(mex, gw, lk, cells):
+    """tci_mex('dram', ...) on TestData cells (the metric's dataset) equals mcmc.dram_run on the same
+    inputs bit for bit: summaries, thinned chain, s2chain and the final proposal factor, for the fused
+    and the walk engine; 700 steps with burn-in scaling and four covariance updates."""
+    ids = [0, 3, 17, 42, 101, 150, 222, 298]
+    for engine in ("fused", "walk"):
+        plan, res = _dram_gateway_vs_binding(mex, gw, lk, cells, ids,
+                                             dict(nsimu=700.0, burnintime=300.0, adaptint=100.0, thin=7.0,
+                                                  seed=91.0, method="dram", engine=engine))
+        assert np.all(res["accept_rate"] > 0)
+    # nargout = 1: no chain rows are kept (thin 0), the summaries are the same
+    plan, a = _dram_args(mex, cells, ids)
+    o = _opts(mex, nsimu=700.0, burnintime=300.0, seed=91.0, chain_keys=(np.asarray(plan.cells) * 3 + 11.0))
+    only = mex.call("dram", gw, *a, o, nlhs=1)[0]
+    o.free()
+    np.testing.assert_array_equal(only["mean"], res["mean"])
+    expect("tci:call", mex.call, "dram", gw, np.array([300.0]), *[x[:, :1] for x in a[1:7]], 1.0)  # cell 300 of 299
+
+
+@pytest.mark.gpu
+def test_dram_equals_the_binding_bitwise_at_config4_shape(mex):
+    """The same at BASELINE config 4's shape: 24 synthetic 200-point cells (P = 207, the matrix-core
+    adaptation k_adapt_mfma<8, 13>), through a context the gateway created from a MATLAB data struct."""
+    from transcriptioncycleinference_amd import Likelihood, from_lists
+    from transcriptioncycleinference_amd.construct import builtin_construct
+    from transcriptioncycleinference_amd.data import synthetic_cells
+
+    cs = builtin_construct("P2P-MS2v5-LacZ-PP7v4")
+
+    def fwd(times, theta):
+        nan = [np.full(len(t), np.nan) for t in times]
+        with Likelihood(from_lists([(t, a, a) for t, a in zip(times, nan)]), cs, device=0) as L:
+            return L.forward(theta, np.arange(len(times), dtype=np.int32), grid="interp")
+
+    syn, _ = synthetic_cells(24, 200, 20201028, fwd)
+    d = data_struct(mex, syn, range(syn.n_cells))
+    h = mex.call("create", d, "P2P-MS2v5-LacZ-PP7v4", 0.0)[0]
+    d.free()
+    hp = MxPtr(mex, mex.handle(int(h[0, 0])))
+    try:
+        with Likelihood(syn, cs, device=0) as L:
+            for engine in ("walk", "batched"):
+                _dram_gateway_vs_binding(mex, hp, L, syn, list(range(24)),
+                                         dict(nsimu=500.0, burnintime=200.0, adaptint=100.0, thin=5.0, seed=7.0,
+                                              engine=engine))
+    finally:
+        mex.call("destroy", hp, nlhs=0)
+        hp.free()

@@ -60,7 +60,7 @@ class tci_dram_options(C.Structure):
                 ("updatesigma", C.c_int32), ("drscale", C.c_double), ("adascale", C.c_double),
                 ("qcovadj", C.c_double), ("burnin_scale", C.c_double), ("stats_from", C.c_int64),
                 ("thin", C.c_int64), ("seed", C.c_uint64), ("engine", C.c_int32), ("max_chunk", C.c_int32),
-                ("chain_keys", C.POINTER(C.c_int64))]
+                ("chain_keys", C.POINTER(C.c_int64)), ("adapt_pmax", C.c_int64)]
 
 
 class tci_dram_outputs(C.Structure):

@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "tci_diag.h"
 #include "tci_dram_internal.h"
 #include "tci_internal.h"
 
@@ -603,6 +604,7 @@ int tci_dram_defaults(tci_dram_options* o) {
   o->engine = TCI_DRAM_AUTO;
   o->max_chunk = 0;
   o->chain_keys = nullptr;
+  o->adapt_pmax = 0;
   return TCI_OK;
 }
 
@@ -615,10 +617,11 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
       !qcov_diag || !sigma2_0)
     return fail(ctx, TCI_EINVAL, "tci_dram_run: null argument or no chains");
   if (opt->n_steps < 1 || opt->ntry < 1 || opt->ntry > 2 || opt->adaptint < 0 || !(opt->drscale > 0) ||
-      opt->engine < TCI_DRAM_AUTO || opt->engine > TCI_DRAM_WALK || opt->max_chunk < 0)
+      opt->engine < TCI_DRAM_AUTO || opt->engine > TCI_DRAM_WALK || opt->max_chunk < 0 || opt->adapt_pmax < 0 ||
+      opt->adapt_pmax > TCI_MAX_POINTS + 7)
     return fail(ctx, TCI_EINVAL,
                 "tci_dram_run: bad options (n_steps >= 1, ntry in {1,2}, adaptint >= 0, engine in {0,1,2,3}, "
-                "max_chunk >= 0)");
+                "max_chunk >= 0, 0 <= adapt_pmax <= 2055)");
   int rc = check_rows(ctx, ld, cell_id, n_chains);
   if (rc != TCI_OK) return rc;
   if (ld > TCI_MAX_POINTS + 7) return fail(ctx, TCI_ERANGE, "tci_dram_run: ld too large");
@@ -635,7 +638,9 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
       if (!(qcov_diag[c * L + j] > 0)) return fail(ctx, TCI_EINVAL, "tci_dram_run: qcov_diag must be > 0");
     }
   }
-  const int64_t p_max_all = *std::max_element(npar.begin(), npar.end());  // > 208: k_adapt_gt's tile grid
+  // the P the adaptation kernel is picked for (> 208: k_adapt_gt and its tile grid): this run's largest,
+  // or the whole fit's when this run is a shard of it (adapt_pmax)
+  const int64_t p_max_all = std::max<int64_t>(*std::max_element(npar.begin(), npar.end()), opt->adapt_pmax);
   // limits of the adaptation window, checked before anything is allocated or launched: the
   // adaptation kernel's LDS (the window's run table grows with adaptint) and the chain kernels'
   // 32-bit window-log offsets (adaptint * ld)
@@ -726,7 +731,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_ALLOC(sq_mean, double, n);
   TCI_ALLOC(sq_m2, double, n);
   TCI_ALLOC(step, int64_t, 1);
-#if defined(TCI_CHAIN_PROFILE) || defined(TCI_ADAPT_PROFILE)
+#if TCI_CHAIN_PROFILE || TCI_ADAPT_PROFILE
   TCI_ALLOC(prof, int64_t, 32);
   TCI_HIP(ctx, hipMemsetAsync(st.prof, 0, 32 * sizeof(int64_t), ctx->stream));
 #endif
@@ -783,9 +788,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_HIP(ctx, hipEventCreate(&ev0));
   TCI_HIP(ctx, hipEventCreate(&ev1));
   TCI_HIP(ctx, hipEventRecord(ev0, s));
-  int64_t p_max = 0;
-  for (size_t c = 0; c < n; ++c) p_max = std::max<int64_t>(p_max, npar[c]);
-  p.pmax = p_max;
+  p.pmax = p_max_all;
   // the fused engine's draws pass keeps a chain's R (packed fp32) and a tile of normals and products
   // in LDS: it must fit a CU (160 KB). AUTO picks it whenever it fits: measured on config 4 (10,000
   // chains x 200 points, 39 per CU) its chain walk + draws pass take 209 us per step against 1950 us
@@ -864,7 +867,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
   TCI_HIP(ctx, hipStreamSynchronize(s));
   if (exec) (void)hipGraphExecDestroy(exec);
   if (graph) (void)hipGraphDestroy(graph);
-#if defined(TCI_CHAIN_PROFILE) || defined(TCI_ADAPT_PROFILE)
+#if TCI_CHAIN_PROFILE || TCI_ADAPT_PROFILE
   {
     int64_t ph[32];
     TCI_HIP(ctx, hipMemcpy(ph, st.prof, sizeof(ph), hipMemcpyDeviceToHost));
@@ -873,7 +876,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
     // TCI_ADAPT_PROFILE: thread 0's cycles per adaptation phase. All summed over the chains.
     double rounds = 0.0;
     int nslots = 8;
-#if defined(TCI_CHAIN_PROFILE) && (TCI_CHAIN_PROFILE == 1 || TCI_CHAIN_PROFILE == 3)
+#if TCI_CHAIN_PROFILE == 1 || TCI_CHAIN_PROFILE == 3
     // =3: slots 8 w + k, wave w's cycles per phase (slot 8 w + 5 also counts the rounds)
     nslots = TCI_CHAIN_PROFILE == 3 ? 32 : 8;
     rounds = (double)((uint64_t)ph[5] >> 40) / (double)n;

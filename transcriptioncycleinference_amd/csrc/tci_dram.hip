@@ -1852,7 +1852,7 @@ constexpr int kAdRB = 16;  // window runs per LDS batch
 __host__ __device__ inline int64_t adapt_mfma_lds_bytes(int64_t P, int64_t nb) {
   const int64_t NT = (P + 15) / 16, LX = 16 * NT;
   const int64_t shared = 2 * kAdRB * LX > 2 * NT * 256 ? 2 * kAdRB * LX : 2 * NT * 256;  // X, Xw | panel buffers
-  return (shared + 2 * LX) * 8 + ((2 * nb + 2) * 4 + 7) / 8 * 8;  // + the run starts and flags
+  return (shared + 2 * LX) * 8 + ((nb + 1) * 4 + 7) / 8 * 8;  // + the run starts
 }
 
 template <int NW, int MAXT, int kAdOwn, int WPE = (NW <= 8 ? 2 : NW / 4)>  // kAdOwn: output tiles per wave (a
@@ -1888,7 +1888,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const int nb = (TCI_ADAPT_ABLATE & 2) ? 0 : (int)p.adaptint;
   const double* win = st.window + c * p.win * ld;
   int* rs = (int*)(mo + LX);  // [nb + 1] the window's runs of equal rows: start rows, then nb
-  int* rf = rs + nb + 1;      // [nb] 1 where a run starts
   uint64_t aph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
 #define TCI_APHASE(k) \
   if (TCI_ADAPT_PROFILE) { a1 = stamp(); aph[k] += a1 - a0; a0 = a1; }
@@ -2161,7 +2160,7 @@ __host__ __device__ inline int gt_rows(int64_t P) {  // window rows per LDS batc
 }
 __host__ __device__ inline int64_t adapt_gt_lds_bytes(int64_t P, int64_t nb) {
   const int64_t LX = (P + 15) / 16 * 16;
-  return ((int64_t)gt_rows(P) * LX + 2 * LX) * 8 + ((2 * nb + 2) * 4 + 7) / 8 * 8;  // + the window's runs
+  return ((int64_t)gt_rows(P) * LX + 2 * LX) * 8 + ((nb + 1) * 4 + 7) / 8 * 8;  // + the window's run starts
 }
 // tile k of the row-major upper triangle of an n x n tile grid starting at tile row r0 -> (ti, tj)
 __device__ __forceinline__ void tri_tile(int k, int n, int r0, int& ti, int& tj) {
@@ -2202,7 +2201,6 @@ __global__ __launch_bounds__(64 * kGtWaves) __attribute__((amdgpu_waves_per_eu(4
   const int nb = (int)p.adaptint;
   const double* win = st.window + c * p.win * ld;
   int* rs = (int*)(mo + LX);  // [nb + 1] the window's runs: start rows, then nb
-  int* rf = rs + nb + 1;      // [nb] scratch
   // TCI_ADAPT_PROFILE: thread 0's s_memtime cycles per phase: scatter, merge, diagonal tiles,
   // panel solves, trailing updates, R store
   uint64_t aph[6] = {0, 0, 0, 0, 0, 0}, a0 = stamp(), a1;
@@ -2516,8 +2514,23 @@ int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& k
 }
 int64_t dram_adapt_lds_bytes(int64_t pmax, int64_t adaptint) {
   if (adaptint <= 0) return 0;
-  if (pmax <= 16 * 9 || (pmax <= 16 * 13 && pmax <= kAdaptGtFrom)) return adapt_mfma_lds_bytes(pmax, adaptint);
-  return adapt_gt_lds_bytes(pmax, adaptint);
+  // the kernel dram_launch_adapt picks, its dynamic LDS, plus its static __shared__ (read from the code
+  // object, so a later change to the kernel's static arrays is counted)
+  const void* k;
+  int64_t dyn;
+  if (pmax <= 16 * 9) {
+    k = (const void*)k_adapt_mfma<8, 9, 6, 4>;
+    dyn = adapt_mfma_lds_bytes(pmax, adaptint);
+  } else if (pmax <= 16 * 13 && pmax <= kAdaptGtFrom) {
+    k = (const void*)k_adapt_mfma<8, 13, 12>;
+    dyn = adapt_mfma_lds_bytes(pmax, adaptint);
+  } else {
+    k = (const void*)k_adapt_gt;
+    dyn = adapt_gt_lds_bytes(pmax, adaptint);
+  }
+  hipFuncAttributes a{};
+  const int64_t stat = hipFuncGetAttributes(&a, k) == hipSuccess ? (int64_t)a.sharedSizeBytes : 4096;
+  return dyn + stat;
 }
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl) {
   const int64_t ns = 4 * (rpl <= 2 ? kChainEPW : 1);  // k_chain: evl, yl, xch, xip (and slack)

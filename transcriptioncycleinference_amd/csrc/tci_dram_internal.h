@@ -102,7 +102,8 @@ struct DramParams {
   int64_t stats_from;
   int64_t thin;
   int64_t n_keep;
-  int64_t pmax;        // max parameter count over the chains (picks the adaptation kernel)
+  int64_t pmax;        // max parameter count over the chains, or tci_dram_options.adapt_pmax if larger (picks
+                       // the adaptation kernel)
   int64_t chunk;       // fused engine: rows per chain of the draws buffer (>= the longest chunk)
   int64_t walk;        // fused engine: 1 = one wavefront per chain walks the chunk (k_walk), 0 = k_chain
   int64_t win;         // window rows per chain: adaptint, or (no adaptation) 100; the
@@ -121,9 +122,9 @@ int dram_launch_init_stats(const DramState& st, const DramParams& p, void* strea
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,
                       int64_t s_end, int with_records, void* stream);
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl);  // LDS per workgroup of the fused engine
-// Dynamic LDS of the adaptation kernel dram_launch_adapt picks for (pmax, adaptint): the window's run
-// table grows with adaptint (8 bytes per row), so tci_dram_run refuses an adaptint past the CU's LDS
-// before any launch.
+// LDS of the adaptation kernel dram_launch_adapt picks for (pmax, adaptint), dynamic plus the kernel's
+// static __shared__: the window's run table grows with adaptint (4 bytes per row), so tci_dram_run
+// refuses an adaptint past the CU's LDS before any launch.
 int64_t dram_adapt_lds_bytes(int64_t pmax, int64_t adaptint);
 // The records of the window of chain rows ending at row *st.step (posterior mean / M2, window column
 // sums, s2 statistics, thinned outputs) from the rows every engine logs: run after a window's last

@@ -31,7 +31,7 @@ class Cells:
         self.t = np.ascontiguousarray(self.t, np.float64)
         self.ms2 = np.ascontiguousarray(self.ms2, np.float64)
         self.pp7 = np.ascontiguousarray(self.pp7, np.float64)
-        if self.offsets.ndim != 1 or len(self.offsets) < 2 or self.offsets[0] != 0:
+        if self.offsets.ndim != 1 or len(self.offsets) < 1 or self.offsets[0] != 0:  # [0]: no cells
             raise ValueError("offsets must be [0, ..., total]")
         if np.any(np.diff(self.offsets) < 0) or self.offsets[-1] != len(self.t):
             raise ValueError("offsets must be non-decreasing and end at len(t)")

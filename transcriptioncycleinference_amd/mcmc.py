@@ -56,6 +56,7 @@ class DramOptions:
     seed: int = 20201028
     engine: str = "auto"          # "auto" | "fused" | "batched" | "walk" (include/tci.h TCI_DRAM_*): identical chains
     max_chunk: int = 0            # FUSED/WALK rows per draws pass + walk (0 = automatic); identical chains
+    adapt_pmax: int = 0           # a shard of a larger fit: that fit's largest P (the adaptation kernel's pick)
 
     ENGINES = {"auto": 0, "fused": 1, "batched": 2, "walk": 3}
 
@@ -67,7 +68,8 @@ class DramOptions:
                                      int(bool(self.updatesigma)), float(self.drscale), float(self.adascale),
                                      float(self.qcovadj), float(self.burnin_scale), int(self.stats_from),
                                      int(self.thin), int(self.seed) & 0xFFFFFFFFFFFFFFFF,
-                                     self.ENGINES[self.engine], int(self.max_chunk), _lib.ptr(chain_keys, _lib._i64p))
+                                     self.ENGINES[self.engine], int(self.max_chunk), _lib.ptr(chain_keys, _lib._i64p),
+                                     int(self.adapt_pmax))
 
 
 @dataclass
@@ -154,6 +156,7 @@ class FitResult:
     gather_s: float = 0.0                      # parallel.fit_sharded: wall time of the results all-gather
     gather_bytes: int = 0                      # parallel.fit_sharded: bytes every rank receives in it
     local: Optional["FitResult"] = None        # parallel.fit_sharded: this rank's own fit (raw chains, final_theta)
+    rows_per_lane_uniform: bool = True         # parallel.fit_sharded: every rank ran the same likelihood variant
 
 
 @dataclass
@@ -190,6 +193,27 @@ class FitPlan:
     approved: List[int]       # MCMCresults.ApprovedFits per fitted cell (:345-350)
 
 
+def _previous(v0, approved, g: int):
+    """(skip, v0 of the cell or None, ApprovedFits) for dataset-wide 0-based cell ``g`` (:193-198, :345-350)."""
+    prev = _per_cell(v0, g)
+    a = 0
+    if isinstance(prev, PreviousFit):
+        a = int(prev.ApprovedFits)
+        prev = prev.mean_v
+    if v0 is not None and (prev is None or np.size(prev) != 1 or not np.isfinite(float(prev))):
+        return True, None, a
+    ap = _per_cell(approved, g)
+    if ap is not None:
+        a = int(ap)
+    return False, (None if v0 is None else float(prev)), a
+
+
+def kept_cells(cl: Cells, ids: Sequence[int], v0=None, cell_offset: int = 0) -> List[int]:
+    """The cells of ``ids`` that get a chain: those with a previous entry when ``v0`` is given
+    (:196-198), all of them otherwise -- :func:`plan_fit`'s rule, without drawing anything."""
+    return [int(c) for c in ids if not _previous(v0, None, int(cell_offset) + int(c))[0]]
+
+
 def plan_fit(cl: Cells, ids: Sequence[int], seed: int, ratePriorWidth: float = 50.0, v0=None,
              approved=None, cell_offset: int = 0) -> FitPlan:
     """The parfor body's per-cell setup for the cells ``ids`` (host only, no GPU).
@@ -207,17 +231,9 @@ def plan_fit(cl: Cells, ids: Sequence[int], seed: int, ratePriorWidth: float = 5
         c = int(c)
         t = cl.cell(c)[0]
         g = int(cell_offset) + c
-        prev = _per_cell(v0, g)
-        a = 0
-        if isinstance(prev, PreviousFit):
-            a = int(prev.ApprovedFits)
-            prev = prev.mean_v
-        if v0 is not None and (prev is None or np.size(prev) != 1 or not np.isfinite(float(prev))):
+        skip, vv, a = _previous(v0, approved, g)
+        if skip:
             continue
-        ap = _per_cell(approved, g)
-        if ap is not None:
-            a = int(ap)
-        vv = None if v0 is None else float(prev)
         rows.append(cell_setup(t, np.random.default_rng([int(seed), g]), ratePriorWidth, vv))
         keep.append(c)
         appr.append(a)

@@ -168,14 +168,21 @@ def fit_sharded(lk, group=None, device: Optional[str] = None, v0=None, approved=
     cells (its own GPU-resident DRAM chains), then ONE all-gather of the packed per-cell results
     (RCCL on GPUs, gloo on CPU) gives every rank the whole dataset's ``MCMCresults`` / ``MCMCplot``
     (the parfor's sliced-output assembly, :315-356). The chains' randomness is keyed by the
-    dataset-wide cell index (:func:`mcmc.fit`), so the gathered results equal a one-GPU fit of all
-    cells bit for bit.
+    dataset-wide cell index (:func:`mcmc.fit`), and every rank adapts with the kernel the whole fit's
+    largest P picks (``DramOptions.adapt_pmax``, all-reduced), so the gathered results equal a
+    one-GPU fit of all cells bit for bit -- provided every rank's ``Likelihood`` runs the kernel
+    variant the one-GPU one does (``lk.info['rows_per_lane']``, set by the context's longest cell:
+    the SS's lane sums follow it). Shards whose longest cells differ in that variant give a valid fit
+    whose chains are not bitwise the one-GPU chains; ``rows_per_lane_uniform`` in the result says
+    which case a run was.
 
     Two layouts:
     * ``cell_offset=None``: every rank holds the whole dataset in ``lk`` and fits the contiguous
       range ``shard_bounds`` gives it (balanced by Σ N_c·W̄);
     * ``cell_offset=k``: ``lk`` holds only this rank's contiguous block of the dataset, starting at
       dataset-wide index k (each rank loaded its own shard files); every cell of ``lk`` is fitted.
+      A rank with no cells (more ranks than shards) passes ``lk=None``: it fits nothing but takes
+      part in every collective, so the other ranks never wait on it.
 
     ``v0`` / ``approved``: per-cell inputs over ALL cells (by 1-based cell_index in a mapping, or
     0-based in a sequence); ``fit`` reads them by dataset-wide cell, so every shard passes them
@@ -187,19 +194,37 @@ def fit_sharded(lk, group=None, device: Optional[str] = None, v0=None, approved=
     import torch
     import torch.distributed as dist
 
-    from .mcmc import fit
+    import dataclasses
+
+    from .mcmc import DramOptions, fit, kept_cells
 
     on = dist.is_available() and dist.is_initialized()
     world, rank = (dist.get_world_size(group), dist.get_rank(group)) if on else (1, 0)
-    cl = lk.cells
-    if cell_offset is None:
+    if lk is None and cell_offset is None:
+        raise ValueError("fit_sharded: lk=None (a rank without cells) needs the cell_offset layout")
+    cl = lk.cells if lk is not None else None
+    if cl is None:
+        ids, off = [], int(cell_offset)
+    elif cell_offset is None:
         b = shard_bounds(cell_weights(cl, lk.construct.L0, v0), world)
         ids, off = list(range(int(b[rank]), int(b[rank + 1]))), 0
     else:
         ids, off = list(range(cl.n_cells)), int(cell_offset)
-    fr = fit(lk, cells=ids, v0=v0, approved=approved, cell_offset=off, **fit_kwargs) if ids else None
-    n_max = int(np.max(cl.lengths)) if cl.n_cells else 0
     dev = torch.device(device) if device else torch.device("cpu")
+    # the whole fit's largest P (over the cells that get a chain) and kernel variant, over the ranks
+    kept = kept_cells(cl, ids, v0, off)
+    pmax = 7 + int(np.max(cl.lengths[kept])) if kept else 0
+    rpl = int(lk.info["rows_per_lane"]) if kept else -1
+    rpl_lo, rpl_hi = (rpl, rpl) if kept else (1 << 30, -1)
+    if on:
+        t = torch.tensor([pmax, rpl_hi, -rpl_lo], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        pmax, rpl_hi, rpl_lo = int(t[0].item()), int(t[1].item()), -int(t[2].item())
+    opts = fit_kwargs.pop("opts", None)
+    opts = dataclasses.replace(opts) if opts is not None else DramOptions()
+    opts.adapt_pmax = max(int(opts.adapt_pmax), pmax)
+    fr = fit(lk, cells=ids, v0=v0, approved=approved, cell_offset=off, opts=opts, **fit_kwargs) if ids else None
+    n_max = int(np.max(cl.lengths)) if cl is not None and cl.n_cells else 0
     if on and cell_offset is not None:  # shards may differ in their longest cell: one common width
         t = torch.tensor([n_max], dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
@@ -217,6 +242,11 @@ def fit_sharded(lk, group=None, device: Optional[str] = None, v0=None, approved=
         dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         ev, ms = int(t[1].item()), float(mx[0].item())
+    if cl is None:  # no cells here: the other ranks' rows, without data columns
+        from .data import from_lists
+
+        cl = from_lists([], "empty-shard")
     out = unpack_results(rows, cl, cl.name, int(ev), float(ms), cell_offset=off)
     out.gather_s, out.gather_bytes, out.local = gather_s, int(rows.nbytes), fr
+    out.rows_per_lane_uniform = rpl_lo >= rpl_hi   # no rank fitted anything, or all ran one variant
     return out
