@@ -36,6 +36,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+FP64_PEAK_TFS = 78.6   # MI355X FP64 dense peak, vector and MFMA alike: 1024 SIMDs x 32 FLOP/clk x 2.4 GHz (a
+                       # v_mfma_f64_16x16x4, 2,048 FLOP, issues every 64 cycles: DESIGN.md §7, r05q)
 SIMDS = 256 * 4        # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9       # max engine clock (MI355X_MICROARCH.md)
 CONSTRUCT = "P2P-MS2v5-LacZ-PP7v4"
@@ -224,6 +226,7 @@ def end_to_end(lk, n_steps: int, seed: int, reduce=None):
     t0 = time.perf_counter()
     fr = fit(lk, n_steps=n_steps, n_burn=max(1, n_steps // 20), seed=seed)
     wall = time.perf_counter() - t0
+    roof = sampler_roofline(lk, n_steps=2000, label="TestData: ")   # untimed, after the fit
     dev_s, evals, chains = fr.elapsed_ms * 1e-3, int(fr.n_evals), len(fr.MCMCresults)
     if reduce is not None:
         dev_s, wall = reduce(dev_s, "max"), reduce(wall, "max")
@@ -233,7 +236,7 @@ def end_to_end(lk, n_steps: int, seed: int, reduce=None):
             "value_basis": "wall",
             "us_per_step": wall * 1e6 / max(n_steps - 1, 1),
             "device_value": evals / dev_s, "device_us_per_step": dev_s * 1e6 / max(n_steps - 1, 1),
-            "accept_rate_median_rank0": float(np.median(fr.accept_rate))}
+            "accept_rate_median_rank0": float(np.median(fr.accept_rate)), "roofline_rank0": roof}
 
 
 CONFIG_SHARDS = 8            # the 10,000 synthetic cells are 8 shards of 1,250
@@ -388,6 +391,8 @@ def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_s
             ok = ok and bool(np.all(np.isfinite(s_ss)))
         else:
             ok = ok and cells.n_cells == 0   # only a rank without cells has no local fit
+        # untimed: the sampler kernels' roofline on this rank's chains (rank 0's in the line)
+        roof = sampler_roofline(lk, cell_offset=lo, label=f"config{cfg} rank {rank}: ") if cells.n_cells else None
     dev_s = fr.elapsed_ms * 1e-3     # max over ranks (fit_sharded)
     evals = int(fr.n_evals)          # summed over ranks (fit_sharded)
     gather_s = reduce(fr.gather_s, "max")
@@ -405,9 +410,73 @@ def synthetic_end_to_end(cfg: int, rank: int, world: int, device_index: int, n_s
            "gather_collective": "RCCL all-gather" if coll_device and str(coll_device).startswith("cuda") and world > 1
            else ("gloo all-gather" if world > 1 else "none (one rank)"),
            "accept_rate_median": acc,
-           "outputs_finite": bool(reduce(0.0 if ok else 1.0, "sum") == 0.0)}
+           "outputs_finite": bool(reduce(0.0 if ok else 1.0, "sum") == 0.0),
+           "roofline": roof}
     spot = {"cells": cells, "construct": construct, "theta": s_theta, "cid": s_cid, "ss_gpu": s_ss}
     return out, spot
+
+
+def _tri_stride(ld: int) -> int:
+    """Doubles per chain of the packed FP64 R (csrc/tci_dram_internal.h dram_tri_stride)."""
+    return (ld * (ld + 1) // 2 + 127) // 128 * 128
+
+
+def sampler_roofline(lk, cell_offset: int = 0, n_steps: int = 1000, seed: int = 9, label: str = ""):
+    """Roofline of the sampler's three kernel classes: a short fit of every cell of
+    ``lk`` (all chains of the timed fit, burn-in 100 rows so that every later window is a full covupd +
+    Cholesky, as in 95 % of a 200k-step fit) with HIP events around each launch (tci_dram_options.
+    kernel_times), and the ALGORITHMIC bytes / FLOP per launch of each class from the shapes:
+      draws (k_draws): R read once per chain and launch (dram_tri_stride(ld) doubles) + every row's draws
+        written, (2P + 4) doubles; FLOP: z*R for both stages, 2 x P(P+1) per row (upper-triangular matvec);
+      walk (k_walk / k_chain): per row the draws row read ((2P + 4) doubles), the window-log row written (P
+        doubles + s2 + the run flag), and the cell's data (24 N bytes) once per launch; no FLOP count (the
+        SS evaluations are a dependent VALU chain, DESIGN.md §3);
+      adapt (k_adapt_*): per chain the window (adaptint rows of P doubles + run flags), the covariance tiles
+        read and written (2 x NT(NT+1)/2 x 256 doubles), the means (3P doubles) and R written; FLOP: one
+        symmetric rank-1 update per run of equal rows, P(P+1) each (runs ~ 1 + accept rate x adaptint),
+        plus the Cholesky, P^3/3.
+    Fractions of 8 TB/s and of the 78.6 TFLOP/s FP64 peak."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions, dram_run, plan_fit
+
+    cl = lk.cells
+    plan = plan_fit(cl, list(range(cl.n_cells)), seed, cell_offset=cell_offset)
+    n, ld = plan.x0.shape
+    o = DramOptions(n_steps=n_steps, burnintime=100, adaptint=100, stats_from=1, seed=seed, kernel_times=True)
+    r = dram_run(lk, np.array(plan.cells, np.int32), plan.x0, plan.lower, plan.upper, plan.prior_mu, plan.prior_sig,
+                 plan.qcov_diag, 1.0, o, chain_keys=np.array(plan.cells, np.int64) + cell_offset)
+    P = 7 + cl.lengths[plan.cells].astype(np.float64)
+    N = cl.lengths[plan.cells].astype(np.float64)
+    rows = n_steps - 1
+    acc = float(np.mean(r.accept_rate))
+    NT = np.ceil(P / 16)
+    out = {"workload": f"{label}{n} chains, {n_steps} steps (burn-in 100, adaptint 100), HIP events per launch",
+           "peaks": {"hbm_GBs": HBM_PEAK_GBS, "fp64_TFs": FP64_PEAK_TFS}, "accept_rate_mean": acc}
+    names = ("draws", "walk", "adapt")
+    for k, name in enumerate(names):
+        launches = int(r.kernel_launches[k])
+        if launches == 0:
+            continue
+        us = float(r.kernel_ms[k]) * 1e3 / launches
+        if name == "draws":
+            byts = (8 * _tri_stride(ld) * n * launches + rows * 8 * (2 * P + 4).sum()) / launches
+            flop = rows * 2 * (P * (P + 1)).sum() / launches
+        elif name == "walk":
+            byts = (rows * (8 * (2 * P + 4) + 8 * P + 9).sum() + launches * 24 * N.sum()) / launches
+            flop = None
+        else:
+            runs = 1 + acc * 100
+            byts = (100 * 8 * P + 100 + 2 * 8 * 256 * NT * (NT + 1) / 2 + 3 * 8 * P + 8 * P * (P + 1) / 2).sum()
+            flop = (runs * P * (P + 1) + P ** 3 / 3).sum()
+        d = {"launches": launches, "avg_us": us, "alg_bytes_per_launch": float(byts),
+             "achieved_GBs": float(byts) / (us * 1e-6) / 1e9}
+        d["hbm_frac"] = d["achieved_GBs"] / HBM_PEAK_GBS
+        if flop is not None:
+            d["alg_flop_per_launch"] = float(flop)
+            d["achieved_TFs"] = float(flop) / (us * 1e-6) / 1e12
+            d["fp64_frac"] = d["achieved_TFs"] / FP64_PEAK_TFS
+        d["bound"] = ("fp64" if flop is not None and d["fp64_frac"] > d["hbm_frac"] else "hbm")
+        out[name] = d
+    return out
 
 
 def cpu_baseline_synth(cfg: int, spot: dict, seconds: float):

@@ -163,6 +163,8 @@ typedef struct {
                            shard of: the covariance adaptation kernel is picked by the largest P
                            (k_adapt_gt past 208), so a shard passing the whole fit's value adapts with the
                            same kernel, hence the same bits, as the unsharded fit (parallel.fit_sharded) */
+  int64_t kernel_times; /* 1: time every kernel launch of the FUSED / WALK engines with HIP events on the
+                           launch stream (tci_dram_outputs.kernel_ms); 0 (default): no events */
 } tci_dram_options;
 
 /* DRAM engines; all give identical chains for the same seed.
@@ -197,6 +199,10 @@ typedef struct {
   double* s2chain;      /* [ceil(n_steps/thin)][n_chains] */
   double* qcov_R;       /* [n_chains][ld][ld] final proposal factor R (upper): qcov = R'R (mcmcstat results.qcov) */
   double elapsed_ms;    /* device time of the step loop (HIP events) */
+  double kernel_ms[4];  /* with opt.kernel_times (FUSED / WALK): device ms summed per kernel class -- [0] the
+                           draws pass (k_draws), [1] the chain walk (k_chain / k_walk), [2] the covariance
+                           adaptation (k_adapt_*), [3] unused (0) -- written by tci_dram_run, 0 otherwise */
+  int64_t kernel_launches[4]; /* launches per class behind kernel_ms */
 } tci_dram_outputs;
 
 int tci_dram_defaults(tci_dram_options* opt);

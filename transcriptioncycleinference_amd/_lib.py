@@ -60,13 +60,13 @@ class tci_dram_options(C.Structure):
                 ("updatesigma", C.c_int32), ("drscale", C.c_double), ("adascale", C.c_double),
                 ("qcovadj", C.c_double), ("burnin_scale", C.c_double), ("stats_from", C.c_int64),
                 ("thin", C.c_int64), ("seed", C.c_uint64), ("engine", C.c_int32), ("max_chunk", C.c_int32),
-                ("chain_keys", C.POINTER(C.c_int64)), ("adapt_pmax", C.c_int64)]
+                ("chain_keys", C.POINTER(C.c_int64)), ("adapt_pmax", C.c_int64), ("kernel_times", C.c_int64)]
 
 
 class tci_dram_outputs(C.Structure):
     _fields_ = [("mean", _dp), ("std", _dp), ("final_theta", _dp), ("sigma_mean", _dp), ("sigma_std", _dp),
                 ("accept_rate", _dp), ("n_evals", _i64p), ("chain", _dp), ("s2chain", _dp), ("qcov_R", _dp),
-                ("elapsed_ms", C.c_double)]
+                ("elapsed_ms", C.c_double), ("kernel_ms", C.c_double * 4), ("kernel_launches", C.c_int64 * 4)]
 
 
 # (name, restype, argtypes) for every symbol declared in include/tci.h

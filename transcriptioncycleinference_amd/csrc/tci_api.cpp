@@ -605,6 +605,7 @@ int tci_dram_defaults(tci_dram_options* o) {
   o->max_chunk = 0;
   o->chain_keys = nullptr;
   o->adapt_pmax = 0;
+  o->kernel_times = 0;
   return TCI_OK;
 }
 
@@ -808,6 +809,12 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
     p.walk = n_chains > 2 * (int64_t)std::max(n_cu, 1) ? 1 : 0;
   }
   if (fused && !fused_fits) return fail(ctx, TCI_ERANGE, "tci_dram_run: rows too long for the fused engine");
+  for (int k = 0; k < 4; ++k) {
+    out->kernel_ms[k] = 0.0;
+    out->kernel_launches[k] = 0;
+  }
+  tci::LaunchTimer timer;
+  tci::LaunchTimer* tm = opt->kernel_times && fused ? &timer : nullptr;
   if (fused) {
     // Chunks of chain rows up to the next adaptation row (and at most p.chunk rows: the draws
     // buffer holds one chunk); k_chain leaves *st.step at the chunk end. Per chunk: the draws pass
@@ -820,8 +827,8 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
       int64_t end = std::min<int64_t>(opt->n_steps, next + p.chunk - 1);
       end = std::min<int64_t>(end, ((next + win - 1) / win) * win);  // chunks never cross a window
       const int rec = end % win == 0 || end == opt->n_steps;  // the records kept in the chain kernel
-      rc = tci::dram_launch_chain(st, p, ctx->kp, ctx->rpl, next, end, rec, s);
-      if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(st, p, s);
+      rc = tci::dram_launch_chain(st, p, ctx->kp, ctx->rpl, next, end, rec, s, tm);
+      if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(st, p, s, tm);
       next = end + 1;
     }
     e = hipSuccess;
@@ -889,6 +896,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
 #endif
   if (ge != hipSuccess) return hip_fail(ctx, ge, "DRAM step replay");
   if (rc != TCI_OK) return fail(ctx, rc, "DRAM step launch");
+  if (tm) tm->collect(out->kernel_ms, out->kernel_launches);
   float ms = 0.f;
   TCI_HIP(ctx, hipEventElapsedTime(&ms, ev0, ev1));
   (void)hipEventDestroy(ev0);

@@ -1762,7 +1762,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu
 
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
-                   int with_records, hipStream_t stream) {
+                   int with_records, hipStream_t stream, LaunchTimer* timer) {
   const bool wide = p.walk != 0 && draws_walk_wide(st.ld);  // WALK: 64-row draws passes (k_draws<8, 2, 4, 2>)
   const size_t lds = (size_t)draws_lds_bytes(st.ld, wide ? kDrawMTWalk : kDrawMT);
   // 4-wave workgroups, 2 column tiles x 2 row tiles per wave and MFMA call (168 VGPRs: three
@@ -1775,7 +1775,12 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
   const int npass = draws_passes(p.walk != 0);
   const int64_t per_wg = (int64_t)8 * (wide ? kDrawMTWalk : kDrawMT) * npass;  // <= the threads (scalar draws)
   const unsigned gy = (unsigned)((s_end - s_begin + per_wg) / per_wg);
+  if (timer) timer->begin(stream);
   hipLaunchKernelGGL(kd, dim3((unsigned)st.n_chains, gy), dim3(64 * nwd), lds, stream, st, p, s_begin, s_end, npass);
+  if (timer) {
+    timer->end(0, stream);
+    timer->begin(stream);
+  }
   if (p.walk)
     hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + kWalkWaves - 1) / kWalkWaves)),
                        dim3(64 * kWalkWaves), 0, stream, st, p,
@@ -1783,17 +1788,18 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
   else
     hipLaunchKernelGGL((k_chain<RPL, NSEG, (RPL <= 2 ? kChainEPW : 1)>), dim3((unsigned)st.n_chains), dim3(kThreads), 0,
                        stream, st, p, kp, s_begin, s_end, with_records);
+  if (timer) timer->end(1, stream);
   return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;
 }
 
 template <int RPL>
 int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, int64_t a, int64_t b, int rec,
-                   hipStream_t s) {
+                   hipStream_t s, LaunchTimer* timer) {
   switch (kp.n_seg) {
-    case 1: return launch_chain_t<RPL, 1>(st, p, kp, a, b, rec, s);
-    case 2: return launch_chain_t<RPL, 2>(st, p, kp, a, b, rec, s);
-    case 3: return launch_chain_t<RPL, 3>(st, p, kp, a, b, rec, s);
-    case 4: return launch_chain_t<RPL, 4>(st, p, kp, a, b, rec, s);
+    case 1: return launch_chain_t<RPL, 1>(st, p, kp, a, b, rec, s, timer);
+    case 2: return launch_chain_t<RPL, 2>(st, p, kp, a, b, rec, s, timer);
+    case 3: return launch_chain_t<RPL, 3>(st, p, kp, a, b, rec, s, timer);
+    case 4: return launch_chain_t<RPL, 4>(st, p, kp, a, b, rec, s, timer);
     default: return TCI_EINVAL;
   }
 }
@@ -2490,25 +2496,33 @@ int dram_launch_accept1(const DramState& st, const DramParams& p, void* stream) 
 int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream) {
   return launch_stage(k_accept2, st, p, stream);
 }
-int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream) {
+int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream, LaunchTimer* timer) {
+  if (timer) timer->begin((hipStream_t)stream);
+  int rc;
   // P <= 144: 8 waves x 6 tiles at <= 128 VGPRs (two chains per CU): 109.3 -> 105.2 us per
   // TestData adaptation against 4 waves x 12 tiles (r03af; 28 VGPRs spilled, still faster)
-  if (p.pmax <= 16 * 9) return launch_adapt_mfma<8, 9, 6, 4>(st, p, stream);
-  // P <= 208: 8 waves x 12 tiles (16 waves x 6 tiles measured slower)
-  if (p.pmax <= 16 * 13 && p.pmax <= kAdaptGtFrom) return launch_adapt_mfma<8, 13, 12>(st, p, stream);
-  const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax, p.adaptint);
-  if (ensure_dyn_lds((const void*)k_adapt_gt, lds) != TCI_OK) return TCI_EHIP;
-  hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.n_chains), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);
-  return finish();
+  if (p.pmax <= 16 * 9) {
+    rc = launch_adapt_mfma<8, 9, 6, 4>(st, p, stream);
+  } else if (p.pmax <= 16 * 13 && p.pmax <= kAdaptGtFrom) {
+    // P <= 208: 8 waves x 12 tiles (16 waves x 6 tiles measured slower)
+    rc = launch_adapt_mfma<8, 13, 12>(st, p, stream);
+  } else {
+    const size_t lds = (size_t)adapt_gt_lds_bytes(p.pmax, p.adaptint);
+    if (ensure_dyn_lds((const void*)k_adapt_gt, lds) != TCI_OK) return TCI_EHIP;
+    hipLaunchKernelGGL(k_adapt_gt, chain_grid(st.n_chains), dim3(64 * kGtWaves), lds, (hipStream_t)stream, st, p);
+    rc = finish();
+  }
+  if (timer) timer->end(2, (hipStream_t)stream);
+  return rc;
 }
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,
-                      int64_t s_end, int with_records, void* stream) {
+                      int64_t s_end, int with_records, void* stream, LaunchTimer* timer) {
   hipStream_t s = (hipStream_t)stream;
   switch (rpl) {
-    case 1: return launch_chain_r<1>(st, p, kp, s_begin, s_end, with_records, s);
-    case 2: return launch_chain_r<2>(st, p, kp, s_begin, s_end, with_records, s);
-    case 4: return launch_chain_r<4>(st, p, kp, s_begin, s_end, with_records, s);
-    case 8: return launch_chain_r<8>(st, p, kp, s_begin, s_end, with_records, s);
+    case 1: return launch_chain_r<1>(st, p, kp, s_begin, s_end, with_records, s, timer);
+    case 2: return launch_chain_r<2>(st, p, kp, s_begin, s_end, with_records, s, timer);
+    case 4: return launch_chain_r<4>(st, p, kp, s_begin, s_end, with_records, s, timer);
+    case 8: return launch_chain_r<8>(st, p, kp, s_begin, s_end, with_records, s, timer);
     default: return TCI_EINVAL;
   }
 }

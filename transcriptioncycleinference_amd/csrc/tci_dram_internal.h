@@ -1,12 +1,62 @@
 // tci_dram_internal.h -- device state of the GPU-resident batched DRAM sampler.
 #pragma once
 
+#include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <vector>
 
 #include "tci.h"
 #include "tci_internal.h"
 
 namespace tci {
+
+// Optional device time per kernel class (tci_dram_options.kernel_times): a HIP event pair around each
+// launch of the fused / walk engines, on the launch stream, summed after the run's final
+// synchronisation. Classes: 0 the draws pass (k_draws), 1 the chain walk (k_chain / k_walk), 2 the
+// covariance adaptation (k_adapt_*).
+struct LaunchTimer {
+  static constexpr int kClasses = 3;
+  struct Mark {
+    int cls;
+    hipEvent_t a, b;
+  };
+  std::vector<Mark> marks;
+  hipEvent_t open = nullptr;
+  void begin(hipStream_t s) {
+    if (hipEventCreate(&open) == hipSuccess) (void)hipEventRecord(open, s);
+    else open = nullptr;
+  }
+  void end(int cls, hipStream_t s) {
+    hipEvent_t e = nullptr;
+    if (open && hipEventCreate(&e) == hipSuccess) {
+      (void)hipEventRecord(e, s);
+      marks.push_back({cls, open, e});
+    } else if (open) {
+      (void)hipEventDestroy(open);
+    }
+    open = nullptr;
+  }
+  // after the stream is synchronised: total ms and launches per class; releases the events
+  void collect(double* ms, int64_t* launches) {
+    for (Mark& m : marks) {
+      float t = 0.f;
+      if (hipEventElapsedTime(&t, m.a, m.b) == hipSuccess) {
+        ms[m.cls] += t;
+        launches[m.cls] += 1;
+      }
+      (void)hipEventDestroy(m.a);
+      (void)hipEventDestroy(m.b);
+    }
+    marks.clear();
+  }
+  ~LaunchTimer() {
+    for (Mark& m : marks) {
+      (void)hipEventDestroy(m.a);
+      (void)hipEventDestroy(m.b);
+    }
+  }
+};
 
 // One workgroup (256 threads) per chain. All arrays are indexed by chain c; vectors have stride ld (= max parameter count P_max),
 // matrices stride ld*ld (row-major, P_c x P_c used).
@@ -114,13 +164,14 @@ int dram_launch_init(const DramState& st, const double* qcov_diag, const double*
 int dram_launch_propose1(const DramState& st, const DramParams& p, void* stream);
 int dram_launch_accept1(const DramState& st, const DramParams& p, void* stream);
 int dram_launch_accept2(const DramState& st, const DramParams& p, void* stream);
-int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream);  // no-op unless step % adaptint == 0
+int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream,
+                      LaunchTimer* timer = nullptr);  // no-op unless step % adaptint == 0
 int dram_launch_step_incr(const DramState& st, void* stream);
 int dram_launch_init_stats(const DramState& st, const DramParams& p, void* stream);
 // Fused engine: chain rows s_begin..s_end (each chain's ssfun inside the kernel); leaves *st.step = s_end.
 // with_records: s_end ends a window (or the run) -- the window's records are kept by the same kernel.
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,
-                      int64_t s_end, int with_records, void* stream);
+                      int64_t s_end, int with_records, void* stream, LaunchTimer* timer = nullptr);
 int64_t dram_chain_lds_bytes(int64_t ld, int rpl);  // LDS per workgroup of the fused engine
 // LDS of the adaptation kernel dram_launch_adapt picks for (pmax, adaptint), dynamic plus the kernel's
 // static __shared__: the window's run table grows with adaptint (4 bytes per row), so tci_dram_run

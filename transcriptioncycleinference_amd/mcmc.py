@@ -57,6 +57,7 @@ class DramOptions:
     engine: str = "auto"          # "auto" | "fused" | "batched" | "walk" (include/tci.h TCI_DRAM_*): identical chains
     max_chunk: int = 0            # FUSED/WALK rows per draws pass + walk (0 = automatic); identical chains
     adapt_pmax: int = 0           # a shard of a larger fit: that fit's largest P (the adaptation kernel's pick)
+    kernel_times: bool = False    # FUSED/WALK: HIP-event device time per kernel class (DramResult.kernel_ms)
 
     ENGINES = {"auto": 0, "fused": 1, "batched": 2, "walk": 3}
 
@@ -69,7 +70,7 @@ class DramOptions:
                                      float(self.qcovadj), float(self.burnin_scale), int(self.stats_from),
                                      int(self.thin), int(self.seed) & 0xFFFFFFFFFFFFFFFF,
                                      self.ENGINES[self.engine], int(self.max_chunk), _lib.ptr(chain_keys, _lib._i64p),
-                                     int(self.adapt_pmax))
+                                     int(self.adapt_pmax), int(bool(self.kernel_times)))
 
 
 @dataclass
@@ -85,6 +86,8 @@ class DramResult:
     s2chain: Optional[np.ndarray]
     elapsed_ms: float
     qcov_R: Optional[np.ndarray] = None   # final proposal factor (upper, R'R = mcmcstat results.qcov)
+    kernel_ms: Optional[np.ndarray] = None        # DramOptions.kernel_times: ms per class (draws, walk, adapt, -)
+    kernel_launches: Optional[np.ndarray] = None  # and launches per class
 
 
 def dram_run(lk, cell_id, theta0, lower, upper, prior_mu, prior_sig, qcov_diag, sigma2_0,
@@ -108,7 +111,7 @@ def dram_run(lk, cell_id, theta0, lower, upper, prior_mu, prior_sig, qcov_diag, 
     out = _lib.tci_dram_outputs(_lib.ptr(mean, _lib._dp), _lib.ptr(std, _lib._dp), _lib.ptr(fin, _lib._dp),
                                 _lib.ptr(smean, _lib._dp), _lib.ptr(sstd, _lib._dp), _lib.ptr(acc, _lib._dp),
                                 _lib.ptr(nev, _lib._i64p), _lib.ptr(chain, _lib._dp), _lib.ptr(s2c, _lib._dp),
-                                _lib.ptr(qR, _lib._dp), 0.0)
+                                _lib.ptr(qR, _lib._dp), 0.0)   # kernel_ms / kernel_launches: zero-initialised
     keys = None if chain_keys is None else np.ascontiguousarray(chain_keys, np.int64)
     if keys is not None and keys.shape != (n,):
         raise ValueError("chain_keys must have one entry per chain")
@@ -116,7 +119,8 @@ def dram_run(lk, cell_id, theta0, lower, upper, prior_mu, prior_sig, qcov_diag, 
     P = lambda a: _lib.ptr(a, _lib._dp)  # noqa: E731
     lk._check(lk._lib.tci_dram_run(lk._h, C.byref(o), n, _lib.ptr(cid, _lib._i32p), P(theta0), P(lower), P(upper),
                                    P(prior_mu), P(prior_sig), P(qcov_diag), P(s20), ld, C.byref(out)))
-    return DramResult(mean, std, fin, smean, sstd, acc, nev, chain, s2c, float(out.elapsed_ms), qR)
+    return DramResult(mean, std, fin, smean, sstd, acc, nev, chain, s2c, float(out.elapsed_ms), qR,
+                      np.array(out.kernel_ms[:], np.float64), np.array(out.kernel_launches[:], np.int64))
 
 
 # ---------------------------------------------------------------------------
