@@ -262,6 +262,49 @@ __device__ __forceinline__ double row_sum(const double2* KJ, int r, double rd, i
   return fma(kvd, Mc, fma(-ka, C, full));
 }
 
+// The {K, J} table of eval_wave. RPL >= 4: stored TRANSPOSED by residue -- entry e = RPL * lane + t
+// (t wave-uniform, >= -64 RPL) at slot (u mod RPL) * kKJS + u / RPL, u = e + 65 RPL -- so a wave's
+// accesses to entries RPL * lane + t are 64 consecutive 16-B slots, conflict-free for ds_read_b128
+// and ds_write_b128, where the plain layout puts them RPL slots apart (4-way bank conflicts at
+// RPL = 4, 8-way at 8: the MI355X_MICROARCH.md §LDS lane groups). Config 4's walk (RPL = 4):
+// 4,166 -> 3,894 us per launch, bitwise equal (r06g). RPL <= 2 keeps the plain layout: its 2-way
+// conflicts cost less than the slot arithmetic (TestData bench launch 35.8 plain vs 36.6 us
+// transposed, k_chain 218.6 vs 222.5 us per chunk, r06g). Pure addressing: the same entries, the
+// same bits. Needs (2 * 64 + 1) RPL slots: eval_lds_doubles. TCI_KJ_LINEAR=1: plain at every RPL
+// (the A/B).
+#ifndef TCI_KJ_LINEAR
+#define TCI_KJ_LINEAR 0
+#endif
+template <int RPL>
+struct KJTable {
+  static constexpr bool kPlain = TCI_KJ_LINEAR || RPL <= 2;
+  static constexpr int kOff = 65 * RPL;  // u = e + kOff >= RPL for every entry a row reads
+  static constexpr int kKJS = 129;       // slots per residue (u / RPL <= 128)
+  static constexpr int kLg = RPL == 1 ? 0 : RPL == 2 ? 1 : RPL == 4 ? 2 : 3;
+  double2* base;                         // this lane's slot 0 of residue 0 (transposed) / entry RPL * lane (plain)
+  __device__ __forceinline__ KJTable(double* lds, int lane)
+      : base(reinterpret_cast<double2*>(lds) + (kPlain ? RPL * lane + kOff : lane)) {}
+  // slot of this lane's entry RPL * lane + t, relative to base (t uniform: scalar arithmetic)
+  __device__ __forceinline__ int slot(int t) const {
+    if (kPlain) return t;
+    const int T = t + kOff;
+    return (T & (RPL - 1)) * kKJS + (T >> kLg);
+  }
+  __device__ __forceinline__ double2 at(int t) const { return base[slot(t)]; }
+  __device__ __forceinline__ void put(int t, double2 v) { base[slot(t)] = v; }
+};
+
+// row_sum on this lane's row RPL * lane + q + 1 of a KJTable (entries RPL * lane + q - n)
+template <int RPL>
+__device__ __forceinline__ double row_sum_t(const KJTable<RPL>& T, int q, double rd, int na, int ne, double kL,
+                                            const SegParams& s, double kvd, double ka) {
+  const double2 A = T.at(q - na), E = T.at(q - ne);
+  const double full = s.phi * fmax(E.x - kL, 0.0);
+  const double C = A.x - E.x;
+  const double Mc = fma(rd, C, -(A.y - E.y));  // sum of m * c_{r-m}, exact
+  return fma(kvd, Mc, fma(-ka, C, full));
+}
+
 template <int MODE>
 __device__ __forceinline__ void write_nan(int lane, int N, int64_t b, double* out0, double* out1, int64_t ld_out) {
   if (MODE == MODE_SS) {
@@ -460,12 +503,12 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
         }
       }
       const double jexcl = wave_incl_scan(js) - js;  // integers < 2^53: exact, as a shifted scan
-      // KJ[i], i in [-SLOTS-RPL, SLOTS): the SLOTS entries below i = 0 are zeros
-      double2* KJ = reinterpret_cast<double2*>(lds) + SLOTS + RPL;
+      // KJ[i], i in [-SLOTS, SLOTS): the SLOTS entries below i = 0 are zeros (KJTable: transposed)
+      KJTable<RPL> KJ(lds, lane);
 #pragma unroll
       for (int q = 0; q < RPL; ++q) {
-        KJ[RPL * lane + q] = make_double2(K[q], jexcl + jloc[q]);
-        KJ[RPL * lane + q - SLOTS] = make_double2(0.0, 0.0);  // [-SLOTS, 0): every index a row reads
+        KJ.put(q, make_double2(K[q], jexcl + jloc[q]));
+        KJ.put(q - SLOTS, make_double2(0.0, 0.0));  // [-SLOTS, 0): every index a row reads
       }
       wave_sync();
       double kvdM[NSEG], kaM[NSEG], kvdP[NSEG], kaP[NSEG];
@@ -480,18 +523,16 @@ __device__ __forceinline__ double eval_wave(const KParams& kp, const EvalIn<RPL>
       for (int q = 0; q < RPL; ++q) {
         const int r = RPL * lane + q + 1;
         const double rd = (double)r;
-        // entries r - n - 1 of this lane's rows as KJl[q - n]: one scalar offset per cut, the row
-        // in the instruction's immediate offset
-        const double2* KJl = KJ + RPL * lane;
-        const double kL = KJl[q - cu.nL].x;  // shared by every segment and dye (L_MS2 = L_PP7)
+        // entries r - n - 1 of this lane's rows: entry RPL * lane + q - n, one scalar slot per cut
+        const double kL = KJ.at(q - cu.nL).x;  // shared by every segment and dye (L_MS2 = L_PP7)
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) {
 #if TCI_ABLATE & 1
-          accM[k][q] = KJ[r].x + (double)cu.nMa[k];
-          accP[k][q] = KJ[r].y + (double)cu.nL;
+          accM[k][q] = KJ.at(q).x + (double)cu.nMa[k];
+          accP[k][q] = KJ.at(q).y + (double)cu.nL;
 #else
-          accM[k][q] = row_sum(KJl, q + 1, rd, cu.nMa[k], cu.nMe[k], kL, sm[k], kvdM[k], kaM[k]);
-          accP[k][q] = row_sum(KJl, q + 1, rd, cu.nPa[k], cu.nPe[k], kL, sp[k], kvdP[k], kaP[k]);
+          accM[k][q] = row_sum_t(KJ, q, rd, cu.nMa[k], cu.nMe[k], kL, sm[k], kvdM[k], kaM[k]);
+          accP[k][q] = row_sum_t(KJ, q, rd, cu.nPa[k], cu.nPe[k], kL, sp[k], kvdP[k], kaP[k]);
 #endif
         }
         // one row's table reads in flight at a time: issued all at once, the 4*NSEG + 1 reads of
