@@ -48,11 +48,6 @@ struct tci_ctx {
   char* h_io = nullptr;
   char* d_io = nullptr;
   size_t cap_io = 0;
-  // SS batches with an active mask can run over their row list (tci::launch_listed), one list per
-  // stream the context is used on: TCI_LK_COMPACT=1 at tci_create (off by default: DESIGN.md
-  // Appendix A, r06e)
-  int compact = 0;
-  std::map<void*, tci::RowList> lists;
   std::string err;
 };
 
@@ -203,49 +198,13 @@ int pick_rpl(int64_t max_points) {
   return 0;
 }
 
-// The row list of `stream`, holding at least B rows; nullptr when the listed form does not apply: it is
-// off, the stream is being captured into a graph (the list's counters alternate call by call, which a
-// replayed graph would not), or its buffers cannot be had.
-tci::RowList* row_list(tci_ctx* ctx, int64_t B, void* stream) {
-  if (!ctx->compact || (ctx->rpl != 1 && ctx->rpl != 2)) return nullptr;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  tci::RowList& L = ctx->lists[stream];
-  const int64_t need = (B + 3) / 4 * 4;
-  if (L.cap < need) {
-    const int64_t cap = std::max<int64_t>(need, 2 * L.cap);
-    if (L.rows) {  // in flight on the stream until it drains
-      (void)hipStreamSynchronize((hipStream_t)stream);
-      (void)hipFree(L.rows);
-      (void)hipFree(L.cids);
-    }
-    L.rows = nullptr;
-    L.cids = nullptr;
-    L.cap = 0;
-    if (hipMalloc(&L.rows, (size_t)cap * 4) != hipSuccess || hipMalloc(&L.cids, (size_t)cap * 4) != hipSuccess) {
-      if (L.rows) (void)hipFree(L.rows);
-      L.rows = nullptr;
-      return nullptr;
-    }
-    if (!L.counters) {
-      if (hipMalloc(&L.counters, 2 * sizeof(uint32_t)) != hipSuccess) return nullptr;
-      if (hipMemset(L.counters, 0, 2 * sizeof(uint32_t)) != hipSuccess) return nullptr;
-      L.cur = 0;
-    }
-    L.cap = cap;
-  }
-  return &L;
-}
-
 int run(tci_ctx* ctx, int mode, const double* theta, int64_t ld, const int32_t* cell, const uint8_t* active,
         int64_t B, double* out0, double* out1, int64_t ld_out, void* stream) {
   TCI_HIP(ctx, hipSetDevice(ctx->device));
   // every cell has >= 2 points, so a row needs >= 9 entries; the kernels read theta[0..6] of a row
   // before they know its cell (tci_kernels.hip)
   if (B > 0 && ld < 9) return fail(ctx, TCI_ERANGE, "ld_theta=" + std::to_string(ld) + " < 9 (7 + at least 2 rates)");
-  tci::RowList* L = mode == tci::MODE_SS && active != nullptr && B > 0 ? row_list(ctx, B, stream) : nullptr;
-  const int rc = L ? tci::launch_listed(ctx->kp, ctx->rpl, theta, ld, cell, active, B, out0, *L, stream)
-                   : tci::launch(ctx->kp, ctx->rpl, mode, theta, ld, cell, active, B, out0, out1, ld_out, stream);
+  const int rc = tci::launch(ctx->kp, ctx->rpl, mode, theta, ld, cell, active, B, out0, out1, ld_out, stream);
   if (rc != TCI_OK) {
     if (rc == TCI_EHIP) return hip_fail(ctx, hipGetLastError(), "kernel launch");
     return fail(ctx, rc, "kernel launch rejected");
@@ -331,7 +290,6 @@ int tci_create(const tci_cells* cells, const tci_construct* construct, int devic
   int rc = check_construct(ctx, construct);
   if (rc != TCI_OK) return bail(rc);
   ctx->device = device;
-  if (const char* e = std::getenv("TCI_LK_COMPACT")) ctx->compact = std::atoi(e) != 0 ? 1 : 0;
   ctx->n_cells = cells->n_cells;
 
   // ---- host precompute of the theta-independent per-cell tables
@@ -455,12 +413,6 @@ int tci_destroy(tci_ctx* ctx) {
                   (void*)ctx->d_out0, (void*)ctx->d_out1})
     if (q) (void)hipFree(q);
   if (ctx->h_io) (void)hipHostFree(ctx->h_io);
-  if (!ctx->lists.empty()) {
-    (void)hipDeviceSynchronize();  // the lists' streams may be the caller's
-    for (auto& kv : ctx->lists)
-      for (void* q : {(void*)kv.second.rows, (void*)kv.second.cids, (void*)kv.second.counters})
-        if (q) (void)hipFree(q);
-  }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return TCI_OK;

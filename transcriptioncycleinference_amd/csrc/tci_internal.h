@@ -81,20 +81,4 @@ int launch(const KParams& kp, int rpl, int mode, const double* theta, int64_t ld
            const int32_t* cell_id, const uint8_t* active, int64_t B, double* out0, double* out1,
            int64_t ld_out, void* stream);
 
-// The in-bounds rows of an SS batch (tci_kernels.hip k_compact_rows), per context and stream: row
-// indices and their cell ids (cap entries, >= the batch rounded up to 4), and two counters used in
-// turn (cur: this call's; the compaction clears the other one for the next call).
-struct RowList {
-  int32_t* rows = nullptr;
-  int32_t* cids = nullptr;
-  uint32_t* counters = nullptr;
-  int64_t cap = 0;
-  int cur = 0;
-};
-
-// SS batch with an active mask, evaluated over its row list: k_compact_rows, then the likelihood
-// kernel over the listed rows only (rpl 1 or 2). B <= list.cap. Rejected rows get +Inf.
-int launch_listed(const KParams& kp, int rpl, const double* theta, int64_t ld_theta, const int32_t* cell_id,
-                  const uint8_t* active, int64_t B, double* out, RowList& list, void* stream);
-
 }  // namespace tci

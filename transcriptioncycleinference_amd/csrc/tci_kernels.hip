@@ -27,60 +27,43 @@ constexpr int waves_per_block() { return RPL <= 2 ? 1 : 4; }
 // 8; the LDS of a 4-wave block caps RPL = 4 at 4 waves/SIMD anyway).
 constexpr int lk_waves_per_eu(int rpl, int nseg) { return rpl * nseg <= 2 ? 8 : 6; }
 
-// Waves per block of the row-list form (LIST): every wave of a block evaluates (the rejected rows are
-// not in the list), so a block's LDS is never held by a wave that has ended.
-constexpr int kListWaves = 4;
-
-template <int RPL, int NSEG, int MODE, bool LIST>
-__global__ __launch_bounds__(64 * (LIST ? kListWaves : waves_per_block<RPL>())) __attribute__((amdgpu_waves_per_eu(lk_waves_per_eu(RPL, NSEG)))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
+template <int RPL, int NSEG, int MODE>
+__global__ __launch_bounds__(64 * waves_per_block<RPL>()) __attribute__((amdgpu_waves_per_eu(lk_waves_per_eu(RPL, NSEG)))) void tci_cohort_kernel(const KParams kp, const double* __restrict__ theta,
                                                          int64_t ld, const int32_t* __restrict__ cell_id,
                                                          const uint8_t* __restrict__ active, int64_t B,
                                                          double* __restrict__ out0, double* __restrict__ out1,
-                                                         int64_t ld_out, int64_t flag_words,
-                                                         const int32_t* __restrict__ lrows,
-                                                         const int32_t* __restrict__ lcids,
-                                                         const uint32_t* __restrict__ lcount) {
+                                                         int64_t ld_out, int64_t flag_words) {
   constexpr int WAVE_DOUBLES = eval_lds_doubles<RPL>();  // {K,J} table / the two sim rows
-  constexpr int kWavesPerBlock = LIST ? kListWaves : waves_per_block<RPL>();
+  constexpr int kWavesPerBlock = waves_per_block<RPL>();
   __shared__ __attribute__((aligned(16))) double s_lds[kWavesPerBlock][WAVE_DOUBLES];
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t b = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  if (b >= B) return;
   double* lds = s_lds[wid];
-  int64_t b;
-  int c;
-  if constexpr (LIST) {
-    // ---- the i-th in-bounds row of the batch (k_compact_rows): the list's length, the row and its
-    //      cell id in one round trip (the slots past the length are inside the list's allocation)
-    const int64_t i = (int64_t)blockIdx.x * kWavesPerBlock + wid;
-    const uint32_t n = *lcount;
-    const int32_t bi = lrows[i], ci = lcids[i];
-    if (i >= (int64_t)n) return;
-    b = __builtin_amdgcn_readfirstlane(bi);
-    c = __builtin_amdgcn_readfirstlane(ci);
-  } else {
-    b = (int64_t)blockIdx.x * kWavesPerBlock + wid;
-    if (b >= B) return;
 #if TCI_ABLATE & 32
-    if (lane == 0) out0[b] = 1.0;  // launch floor (diagnostics only)
-    return;
+  if (lane == 0) out0[b] = 1.0;  // launch floor (diagnostics only)
+  return;
 #endif
-    // ---- the row's cell id and active flag, then every other load of the evaluation at once. (Also
-    //      reading the theta scalars with the cell id, one round trip earlier, measured no faster and
-    //      fetched the theta lines of the bounds-rejected rows too: DESIGN.md §3.)
-    c = __builtin_amdgcn_readfirstlane(cell_id[b]);
-    // the flag through the scalar cache (one s_load_dword of its 4-byte word): a rejected row's wave
-    // ends without queueing behind the other waves' vector loads (34.2 vs 35.4 us per bench launch,
-    // r05h). flag_words: the rows whose whole word lies inside `active` (which is 4-byte aligned);
-    // the last partial word and a misaligned array read the byte.
-    bool act = true;
-    if (MODE == MODE_SS && active != nullptr)
-      act = b < flag_words ? ((reinterpret_cast<const uint32_t*>(active)[b >> 2] >> (8 * (b & 3))) & 0xffu) != 0
-                           : active[b] != 0;
-    if (!act) {
-      if (lane == 0) out0[b] = INFINITY;  // skipped proposal (bounds-rejected by the caller)
-      return;
-    }
+
+  // ---- the row's cell id and active flag, then every other load of the evaluation at once. (Also
+  //      reading the theta scalars with the cell id, one round trip earlier, measured no faster and
+  //      fetched the theta lines of the bounds-rejected rows too: DESIGN.md §3.)
+  const int c = __builtin_amdgcn_readfirstlane(cell_id[b]);
+  // the flag through the scalar cache (one s_load_dword of its 4-byte word): a rejected row's wave
+  // ends without queueing behind the other waves' vector loads (34.2 vs 35.4 us per bench launch,
+  // r05h). flag_words: the rows whose whole word lies inside `active` (which is 4-byte aligned);
+  // the last partial word and a misaligned array read the byte. (Evaluating only a list of the
+  // in-bounds rows, built by a compaction kernel on the stream, measured slower: DESIGN.md
+  // Appendix A, r06e/r06f.)
+  bool act = true;
+  if (MODE == MODE_SS && active != nullptr)
+    act = b < flag_words ? ((reinterpret_cast<const uint32_t*>(active)[b >> 2] >> (8 * (b & 3))) & 0xffu) != 0
+                         : active[b] != 0;
+  if (!act) {
+    if (lane == 0) out0[b] = INFINITY;  // skipped proposal (bounds-rejected by the caller)
+    return;
   }
   if (c < 0 || ((kp.n_cells >> 31) == 0 && c >= (int)kp.n_cells)) {
     write_nan<MODE>(lane, 0, b, out0, out1, ld_out);
@@ -138,61 +121,8 @@ void launch_one(const KParams& kp, const double* theta, int64_t ld, const int32_
   const dim3 block(64 * kWavesPerBlock);
   const dim3 grid((unsigned)((B + kWavesPerBlock - 1) / kWavesPerBlock));
   const int64_t flag_words = active != nullptr && (reinterpret_cast<uintptr_t>(active) & 3) == 0 ? (B & ~(int64_t)3) : 0;
-  hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE, false>), grid, block, 0, stream, kp, theta, ld, cell_id, active,
-                     B, out0, out1, ld_out, flag_words, nullptr, nullptr, nullptr);
-}
-
-// ---- Row lists (SS batches with an active mask). k_compact_rows lists the batch's in-bounds rows
-// (order within a wave's 64 rows kept; the waves' blocks in the order their atomic lands, which no
-// result depends on: every row writes its own SS) with their cell ids, writes +Inf for the rejected
-// rows, and clears the NEXT call's counter (RowList::cur alternates; the previous call's evaluation
-// has finished reading it, same stream). The evaluation then runs only over the list.
-__global__ __launch_bounds__(256) void k_compact_rows(const uint8_t* __restrict__ active,
-                                                      const int32_t* __restrict__ cell_id, int64_t B,
-                                                      double* __restrict__ out0, int32_t* __restrict__ lrows,
-                                                      int32_t* __restrict__ lcids, uint32_t* __restrict__ counters,
-                                                      int cur) {
-  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x == 0) counters[cur ^ 1] = 0u;
-  const bool in = b < B;
-  const bool ok = in && active[b] != 0;
-  const int32_t c = ok ? cell_id[b] : 0;
-  const uint64_t bal = wave_ballot(ok);
-  if (!ok && in) out0[b] = INFINITY;  // skipped proposal (bounds-rejected by the caller)
-  if (bal == 0) return;
-  uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(&counters[cur], (uint32_t)__builtin_popcountll(bal));
-  base = (uint32_t)__shfl((int)base, 0);
-  if (ok) {
-    const uint32_t r = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-    lrows[r] = (int32_t)b;
-    lcids[r] = c;
-  }
-}
-
-template <int RPL, int NSEG>
-int launch_list_seg(const KParams& kp, const double* theta, int64_t ld, const int32_t* cell_id, const uint8_t* active,
-                    int64_t B, double* out0, RowList& L, hipStream_t stream) {
-  hipLaunchKernelGGL(k_compact_rows, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, stream, active, cell_id, B, out0,
-                     L.rows, L.cids, L.counters, L.cur);
-  hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE_SS, true>), dim3((unsigned)((B + kListWaves - 1) / kListWaves)),
-                     dim3(64 * kListWaves), 0, stream, kp, theta, ld, cell_id, active, B, out0, nullptr, 0, 0,
-                     L.rows, L.cids, L.counters + L.cur);
-  L.cur ^= 1;
-  return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;
-}
-
-template <int RPL>
-int launch_list_rpl(const KParams& kp, const double* theta, int64_t ld, const int32_t* cell_id, const uint8_t* active,
-                    int64_t B, double* out0, RowList& L, hipStream_t st) {
-  switch (kp.n_seg) {
-    case 1: return launch_list_seg<RPL, 1>(kp, theta, ld, cell_id, active, B, out0, L, st);
-    case 2: return launch_list_seg<RPL, 2>(kp, theta, ld, cell_id, active, B, out0, L, st);
-    case 3: return launch_list_seg<RPL, 3>(kp, theta, ld, cell_id, active, B, out0, L, st);
-    case 4: return launch_list_seg<RPL, 4>(kp, theta, ld, cell_id, active, B, out0, L, st);
-    default: return TCI_EINVAL;
-  }
+  hipLaunchKernelGGL((tci_cohort_kernel<RPL, NSEG, MODE>), grid, block, 0, stream, kp, theta, ld, cell_id, active, B,
+                     out0, out1, ld_out, flag_words);
 }
 
 template <int RPL, int NSEG>
@@ -504,18 +434,6 @@ int launch_tiled(const KParams& kp, int mode, const double* theta, int64_t ld, c
 }
 
 }  // namespace
-
-int launch_listed(const KParams& kp, int rpl, const double* theta, int64_t ld_theta, const int32_t* cell_id,
-                  const uint8_t* active, int64_t B, double* out, RowList& list, void* stream) {
-  if (B <= 0) return TCI_OK;
-  if (B > list.cap || active == nullptr) return TCI_EINVAL;
-  hipStream_t st = (hipStream_t)stream;
-  switch (rpl) {
-    case 1: return launch_list_rpl<1>(kp, theta, ld_theta, cell_id, active, B, out, list, st);
-    case 2: return launch_list_rpl<2>(kp, theta, ld_theta, cell_id, active, B, out, list, st);
-    default: return TCI_EINVAL;
-  }
-}
 
 int launch(const KParams& kp, int rpl, int mode, const double* theta, int64_t ld_theta, const int32_t* cell_id,
            const uint8_t* active, int64_t B, double* out0, double* out1, int64_t ld_out, void* stream) {
