@@ -17,11 +17,6 @@
 #ifndef TCI_ADAPT_ABLATE
 #define TCI_ADAPT_ABLATE 0
 #endif
-// k_chain's records (prices them; wrong summaries, and bit 2 a different adaptation): bit0 no window
-// column sums (ColAcc::add), bit1 no sigma^2 sums (S2Acc::add), bit2 no window-log row stores.
-#ifndef TCI_CHAIN_ABLATE
-#define TCI_CHAIN_ABLATE 0
-#endif
 // s_memtime cycles per phase into DramState::prof, printed by tci_dram_run: k_chain (1: wave 0's
 // phases, 2: per-wave barrier waits, 3: every wave's phases) / k_adapt_mfma and k_adapt_gt (1:
 // thread 0's phases; k_adapt_mfma's slot 6 is the run listing, window_runs).

@@ -977,18 +977,6 @@ struct ColAcc {
       }
     }
   }
-  // finish() for entry k alone, of column j (any mapping of entries to columns)
-  __device__ void finish_one(const DramState& st, const DramParams& p, int64_t c, int64_t last, int P, int j, int k) {
-    const int64_t ld = st.ld;
-    const double na = (double)max<int64_t>(first - p.stats_from, 0), nb = (double)max<int64_t>(last - sf + 1, 0);
-    double mean = j < P ? st.smean[c * ld + j] : 0.0, m2 = j < P ? st.sm2[c * ld + j] : 0.0;
-    stats_merge(na, nb, K[k], S1[k], S2[k], mean, m2);
-    if (j < P) {
-      st.smean[c * ld + j] = mean;
-      st.sm2[c * ld + j] = m2;
-      st.wsumv[c * ld + j] = ws[k];
-    }
-  }
   // the window's records at its last row `last` (columns jl + 64 k): merged into the running
   // statistics, the column sums kept for the adaptation
   __device__ void finish(const DramState& st, const DramParams& p, int64_t c, int64_t last, int P, int jl) {
@@ -1126,8 +1114,6 @@ __device__ __forceinline__ void launder_lane(int& lane) { asm volatile("" : "+v"
 // steps (r03y). Only EPW = 1 is instantiated; the EPW = 2 instance was bitwise equal to the other
 // engines (tests/test_dram_gpu.py green with it).
 constexpr int kChainEPW = 1;
-constexpr int kDeferRows = 20;  // window-log rows per batch of k_chain's chunk-end column sums
-constexpr int kS2Wave = 3;      // the wave of k_chain's chunk-end s2 sums
 
 
 template <int RPL, int NSEG, int EPW>
@@ -1234,16 +1220,33 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   double dsc = load_sc(s_begin), dscn = 0.0;
   int sbase = 0;  // lane of step s's first scalar draw in dsc (4 (adv - 1) of the previous round)
   int par = 0;
-  // the logs of the rows as they are decided ("Chain records"): kRecWave logs each row (window slot,
-  // run flag, thinned output), kSigWave each row's s2; the window sums of the logged rows -- column
-  // sums and s2 sums -- are taken after the loop from the logs, in row order (the same additions, the
-  // same bits), by all four waves at once, continuing a window begun by an earlier chunk (or by
-  // k_init_stats). In the loop they sat on the record waves ahead of their evaluations, and the round
-  // waits for its slowest wave (r06cp). Slots are consecutive within a chunk (log_slot).
+  // the logs and window sums of the rows as they are decided ("Chain records"): kRecWave's column
+  // sums, kSigWave's s2 sums (lane 0), continuing a window begun by an earlier chunk (or by
+  // k_init_stats); slots are consecutive within a chunk (log_slot)
   const int64_t slot0 = log_slot(p, s_begin) - s_begin;  // slot of row r: slot0 + r
-  const int64_t first0 = win_first(p, s_begin);
-  const bool cont = s_begin != first0;
-
+  ColAcc<NJ> ca;
+  ca.setup(p, s_begin);
+  S2Acc qa{0.0, 0.0, 0.0, 0.0};
+  const bool cont = s_begin != ca.first;
+  if (w == kRecWave) {
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      const int j = lane + 64 * k;
+      const bool in = j < P;
+      ca.ws[k] = cont && in ? st.wsumv[c * ld + j] : 0.0;
+      ca.S1[k] = cont && in ? st.wacc1[c * ld + j] : 0.0;
+      ca.S2[k] = cont && in ? st.wacc2[c * ld + j] : 0.0;
+      // a window continued from an earlier chunk whose row sf is already logged: K = that row
+      ca.K[k] = !in ? 0.0 : !ca.kfirst ? st.smean[c * ld + j]
+                                         : ca.sf < s_begin ? st.window[(c * p.win + log_slot(p, ca.sf)) * ld + j] : 0.0;
+    }
+  }
+  if (w == kSigWave) {
+    qa.sum = cont ? st.s2acc[3 * c + 0] : 0.0;
+    qa.S1 = cont ? st.s2acc[3 * c + 1] : 0.0;
+    qa.S2 = cont ? st.s2acc[3 * c + 2] : 0.0;
+    qa.K = ca.first > 1 ? st.sq_mean[c] : sqrt(st.s2log[c * p.win]);
+  }
   // thinned output rows: the next kept row >= s_begin and its index, advanced as rows are recorded
   // (no division per row); never matched when nothing is kept
   const bool keep_rows = (st.chain_out != nullptr || st.s2_out != nullptr) && p.thin > 0;
@@ -1254,7 +1257,8 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     if (lane == 0) log_run(st, p, c, slot0 + row, f);
 #pragma unroll
     for (int k = 0; k < NJ; ++k)
-      if (!(TCI_CHAIN_ABLATE & 4) && lane + 64 * k < P) wr[lane + 64 * k] = x[k];
+      if (lane + 64 * k < P) wr[lane + 64 * k] = x[k];
+    ca.add(row, x);
     if (row == next_keep) {  // uniform
       if (st.chain_out != nullptr && kkeep < p.n_keep) {
 #pragma unroll
@@ -1267,6 +1271,7 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   };
   auto rec_s2 = [&](int64_t row, double v) {  // kSigWave: the row bookkeeping in every lane, stores by lane 0
     if (lane == 0) s2lg[(int)(slot0 + row)] = v;
+    if (lane == 0) qa.add(v);
     if (row == next_keep) {  // uniform
       if (lane == 0 && st.s2_out != nullptr && kkeep < p.n_keep) st.s2_out[kkeep * st.n_chains + c] = v;
       ++kkeep;
@@ -1462,6 +1467,19 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
     TCI_PHASE(5)
     if (TCI_CHAIN_PROFILE) ph[5] += 1ull << 40;  // round count in the high bits
   }
+#undef TCI_PHASE
+#if TCI_CHAIN_PROFILE == 3  // every phase of every wave: slot 8 w + k
+  if (lane == 0 && st.prof != nullptr)
+    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&st.prof[8 * w + k], (unsigned long long)ph[k]);
+#elif TCI_CHAIN_PROFILE == 2  // per wave: barrier wait (slot w) and eval + prior + exchange (slot 4 + w)
+  if (lane == 0 && st.prof != nullptr) {
+    atomicAdd((unsigned long long*)&st.prof[w], (unsigned long long)ph[3]);
+    atomicAdd((unsigned long long*)&st.prof[4 + w], (unsigned long long)(ph[1] + ph[2]));
+  }
+#else
+  if (TCI_CHAIN_PROFILE && w == 0 && lane == 0 && st.prof != nullptr)
+    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&st.prof[k], (unsigned long long)ph[k]);
+#endif
   // the last round's rows
   if (w == kRecWave) {
     flush_vec();
@@ -1478,99 +1496,27 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       st.nevals[c] = nev;
       if (c == 0) *st.step = s_end;  // the adaptation reads the row it follows
     }
+    if (with_records) {  // the chunk ends a window (or the run): its records
+      ca.finish(st, p, c, s_end, P, lane);
+    } else {  // the window goes on in the next chunk
+#pragma unroll
+      for (int k = 0; k < NJ; ++k) {
+        const int j = lane + 64 * k;
+        if (j < P) {
+          st.wsumv[c * ld + j] = ca.ws[k];
+          st.wacc1[c * ld + j] = ca.S1[k];
+          st.wacc2[c * ld + j] = ca.S2[k];
+        }
+      }
+    }
   }
   if (w == kSigWave) {
     const double x0 = (p.updatesigma && gpend) ? 1.0 / (Gl * (2.0 / ss)) : s2c;
     flush_s2(x0);
-    if (lane == 0) st.sigma2[c] = x0;
-  }
-  // ---- the chunk's sums, from its logs, in row order (the same additions as row by row, the same
-  //      bits), by every wave at once: wave w the column blocks k = w, w + 4, .., wave kS2Wave the
-  //      s2 sums. The logs are kRecWave's and kSigWave's stores: made visible to the workgroup first.
-  __builtin_amdgcn_s_waitcnt(0);  // this wave's log stores complete (vmcnt also counts stores on gfx9)
-  __threadfence_block();
-  __syncthreads();
-  const int nrow = (int)(s_end - s_begin + 1);
-  for (int k = w; k < NJ; k += NW) {  // uniform per wave
-    const int j = lane + 64 * k;
-    const bool in = j < P;
-    ColAcc<1> ca;
-    ca.setup(p, s_begin);
-    const double* wc = wlog + (int)(slot0 + s_begin) * ldi + (in ? j : 0);
-    // ColAcc::add over the rows: ws over every row, K at row sf, S1 / S2 from row sf on (rs: the first
-    // such row of the chunk; each accumulator sees the same operations in the same order)
-    const int rs = (int)min<int64_t>(max<int64_t>(ca.sf - s_begin, 0), nrow);
-    const bool kset = ca.kfirst && ca.sf >= s_begin && ca.sf <= s_end;
-    double ws = cont && in ? st.wsumv[c * ld + j] : 0.0;
-    double S1 = cont && in ? st.wacc1[c * ld + j] : 0.0;
-    double S2 = cont && in ? st.wacc2[c * ld + j] : 0.0;
-    // a window continued from an earlier chunk whose row sf is already logged: K = that row
-    double K = !in ? 0.0 : !ca.kfirst ? st.smean[c * ld + j]
-                                      : ca.sf < s_begin ? st.window[(c * p.win + log_slot(p, ca.sf)) * ld + j] : 0.0;
-    if (kset && in) K = wc[rs * ldi];
-    if (!(TCI_CHAIN_ABLATE & 1)) {
-      for (int rb = 0; rb < nrow; rb += kDeferRows) {
-        double x[kDeferRows];  // every load of the batch issued together (clamped rows, no branches)
-#pragma unroll
-        for (int u = 0; u < kDeferRows; ++u) x[u] = wc[min(rb + u, nrow - 1) * ldi];
-#pragma unroll
-        for (int u = 0; u < kDeferRows; ++u) x[u] = in ? x[u] : 0.0;
-        if (rb + kDeferRows <= nrow && rb >= rs) {  // uniform: the common batch, every row a statistics row
-#pragma unroll
-          for (int u = 0; u < kDeferRows; ++u) {
-            ws = ws + x[u];
-            const double d = x[u] - K;
-            S1 = S1 + d;
-            S2 = fma(d, d, S2);
-          }
-        } else {
-#pragma unroll
-          for (int u = 0; u < kDeferRows; ++u) {
-            if (rb + u < nrow) {  // uniform
-              ws = ws + x[u];
-              if (rb + u >= rs) {  // uniform
-                const double d = x[u] - K;
-                S1 = S1 + d;
-                S2 = fma(d, d, S2);
-              }
-            }
-          }
-        }
-      }
-    }
-    ca.ws[0] = ws;
-    ca.S1[0] = S1;
-    ca.S2[0] = S2;
-    ca.K[0] = K;
-    if (with_records) {  // the chunk ends a window (or the run): its records
-      ca.finish(st, p, c, s_end, P, j);
-    } else if (in) {  // the window goes on in the next chunk
-      st.wsumv[c * ld + j] = ws;
-      st.wacc1[c * ld + j] = S1;
-      st.wacc2[c * ld + j] = S2;
-    }
-  }
-  if (w == kS2Wave) {
-    // S2Acc::add for the chunk's rows in row order: sqrt(s2) - K lane-parallel, 64 rows per pass, the
-    // sums through lane broadcasts (window_s2_records' arithmetic)
-    S2Acc qa{cont ? st.s2acc[3 * c + 0] : 0.0, cont ? st.s2acc[3 * c + 1] : 0.0, cont ? st.s2acc[3 * c + 2] : 0.0,
-             first0 > 1 ? st.sq_mean[c] : sqrt(st.s2log[c * p.win])};
-    if (!(TCI_CHAIN_ABLATE & 2)) {
-      // every lane reads every row (one address per load: a broadcast) and adds them in row order --
-      // no lane broadcasts in the chain
-      const double* lg = s2lg + (int)(slot0 + s_begin);
-      for (int rb = 0; rb < nrow; rb += kDeferRows) {
-        double v[kDeferRows];
-#pragma unroll
-        for (int u = 0; u < kDeferRows; ++u) v[u] = lg[min(rb + u, nrow - 1)];
-#pragma unroll
-        for (int u = 0; u < kDeferRows; ++u)
-          if (rb + u < nrow) qa.add(v[u]);  // uniform
-      }
-    }
     if (lane == 0) {
+      st.sigma2[c] = x0;
       if (with_records) {
-        qa.finish(st, c, first0, s_end);
+        qa.finish(st, c, ca.first, s_end);
       } else {
         st.s2acc[3 * c + 0] = qa.sum;
         st.s2acc[3 * c + 1] = qa.S1;
@@ -1578,20 +1524,6 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
       }
     }
   }
-  TCI_PHASE(7)  // the chunk's epilogue: last logs, sums, records
-#undef TCI_PHASE
-#if TCI_CHAIN_PROFILE == 3  // every phase of every wave: slot 8 w + k
-  if (lane == 0 && st.prof != nullptr)
-    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&st.prof[8 * w + k], (unsigned long long)ph[k]);
-#elif TCI_CHAIN_PROFILE == 2  // per wave: barrier wait (slot w) and eval + prior + exchange (slot 4 + w)
-  if (lane == 0 && st.prof != nullptr) {
-    atomicAdd((unsigned long long*)&st.prof[w], (unsigned long long)ph[3]);
-    atomicAdd((unsigned long long*)&st.prof[4 + w], (unsigned long long)(ph[1] + ph[2]));
-  }
-#else
-  if (TCI_CHAIN_PROFILE && w == 0 && lane == 0 && st.prof != nullptr)
-    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&st.prof[k], (unsigned long long)ph[k]);
-#endif
 }
 
 // One wavefront per chain (the WALK engine: many chains, e.g. configs 4/5's 10,000): the same
