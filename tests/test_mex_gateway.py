@@ -323,3 +323,27 @@ def test_dram_equals_the_binding_bitwise_at_config4_shape(mex):
     finally:
         mex.call("destroy", hp, nlhs=0)
         hp.free()
+
+
+@pytest.mark.gpu
+def test_dram_methods_map_to_mcmcstat_semantics(mex, gw, lk, cells):
+    """options.method as mcmcrun reads it: 'dram' = delayed rejection + adaptation, 'am' = adaptation
+    without delayed rejection, 'dr' = delayed rejection without adaptation, 'mh' = neither -- each
+    equal bit for bit to mcmc.dram_run with the matching ntry / adaptint; the default chain output
+    (two outputs, no 'thin') keeps every row."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions, dram_run
+
+    ids = [5, 60, 199]
+    plan, a = _dram_args(mex, cells, ids)
+    for method, ntry, adaptint in (("am", 1, 100), ("dr", 2, 0), ("mh", 1, 0), ("DRAM", 2, 100)):
+        o = _opts(mex, nsimu=400.0, burnintime=150.0, adaptint=100.0, seed=3.0, method=method)
+        res, ch = mex.call("dram", gw, *a, o, nlhs=2)
+        o.free()
+        want = dram_run(lk, np.asarray(plan.cells, np.int32), plan.x0, plan.lower, plan.upper, plan.prior_mu,
+                        plan.prior_sig, plan.qcov_diag, 1.0,
+                        DramOptions(n_steps=400, burnintime=150, adaptint=adaptint, ntry=ntry, stats_from=150, thin=1,
+                                    seed=3))
+        np.testing.assert_array_equal(res["mean"], want.mean.T, err_msg=method)
+        np.testing.assert_array_equal(res["accept_rate"][0], want.accept_rate, err_msg=method)
+        assert ch.shape == (plan.x0.shape[1], len(ids), 400)
+        np.testing.assert_array_equal(np.transpose(ch, (2, 1, 0)), want.chain, err_msg=method)
