@@ -428,9 +428,11 @@ def sampler_roofline(lk, cell_offset: int = 0, n_steps: int = 1000, seed: int = 
     kernel_times), and the ALGORITHMIC bytes / FLOP per launch of each class from the shapes:
       draws (k_draws): R read once per chain and launch (dram_tri_stride(ld) doubles) + every row's draws
         written, (2P + 4) doubles; FLOP: z*R for both stages, 2 x P(P+1) per row (upper-triangular matvec);
+        the split form (k_chain's engine, DESIGN.md §7) reads the row's 2P normals too and writes 2P;
       walk (k_walk / k_chain): per row the draws row read ((2P + 4) doubles), the window-log row written (P
         doubles + s2 + the run flag), and the cell's data (24 N bytes) once per launch; no FLOP count (the
-        SS evaluations are a dependent VALU chain, DESIGN.md §3);
+        SS evaluations are a dependent VALU chain); the split form's k_chain launch also
+        writes the next chunk's normals and scalar draws, (2P + 4) doubles per row;
       adapt (k_adapt_*): per chain the window (adaptint rows of P doubles + run flags), the covariance tiles
         read and written (2 x NT(NT+1)/2 x 256 doubles), the means (3P doubles) and R written; FLOP: one
         symmetric rank-1 update per run of equal rows, P(P+1) each (runs ~ 1 + accept rate x adaptint),
@@ -449,8 +451,10 @@ def sampler_roofline(lk, cell_offset: int = 0, n_steps: int = 1000, seed: int = 
     rows = n_steps - 1
     acc = float(np.mean(r.accept_rate))
     NT = np.ceil(P / 16)
+    split = int(r.kernel_launches[3]) > 0  # the split draws (its first-chunk launch is class 3)
     out = {"workload": f"{label}{n} chains, {n_steps} steps (burn-in 100, adaptint 100), HIP events per launch",
-           "peaks": {"hbm_GBs": HBM_PEAK_GBS, "fp64_TFs": FP64_PEAK_TFS}, "accept_rate_mean": acc}
+           "peaks": {"hbm_GBs": HBM_PEAK_GBS, "fp64_TFs": FP64_PEAK_TFS}, "accept_rate_mean": acc,
+           "split_draws": split}
     names = ("draws", "walk", "adapt")
     for k, name in enumerate(names):
         launches = int(r.kernel_launches[k])
@@ -458,10 +462,11 @@ def sampler_roofline(lk, cell_offset: int = 0, n_steps: int = 1000, seed: int = 
             continue
         us = float(r.kernel_ms[k]) * 1e3 / launches
         if name == "draws":
-            byts = (8 * _tri_stride(ld) * n * launches + rows * 8 * (2 * P + 4).sum()) / launches
+            byts = (8 * _tri_stride(ld) * n * launches + rows * 8 * ((4 * P) if split else (2 * P + 4)).sum()) / launches
             flop = rows * 2 * (P * (P + 1)).sum() / launches
         elif name == "walk":
-            byts = (rows * (8 * (2 * P + 4) + 8 * P + 9).sum() + launches * 24 * N.sum()) / launches
+            per_row = 8 * (2 * P + 4) + 8 * P + 9 + (8 * (2 * P + 4) if split else 0)
+            byts = (rows * per_row.sum() + launches * 24 * N.sum()) / launches
             flop = None
         else:
             runs = 1 + acc * 100

@@ -171,7 +171,9 @@ typedef struct {
  *   FUSED:   per chunk of steps (up to the next adaptation) one wide launch draws every
  *            state-independent random quantity (proposal offsets z*R on MFMA, uniforms, Gamma
  *            variates), then one workgroup per chain walks the chunk with its ssfun evaluations in
- *            the loop (one workgroup barrier per step): latency-bound runs (few chains).
+ *            the loop (one workgroup barrier per step): latency-bound runs (few chains). The draws
+ *            that do not need the adapted R (normals, uniforms, Gamma variates) are drawn on a
+ *            second stream one chunk ahead, under the previous chunk's walk.
  *   BATCHED: one launch per stage, every chain's ssfun in the batched likelihood kernel, replayed
  *            as a hipGraph per adaptation window: many chains, or cells too long for FUSED.
  *   WALK:    FUSED's draws pass, then ONE WAVEFRONT per chain walks the chunk (stage 2 evaluated
@@ -201,7 +203,9 @@ typedef struct {
   double elapsed_ms;    /* device time of the step loop (HIP events) */
   double kernel_ms[4];  /* with opt.kernel_times (FUSED / WALK): device ms summed per kernel class -- [0] the
                            draws pass (k_draws), [1] the chain walk (k_chain / k_walk), [2] the covariance
-                           adaptation (k_adapt_*), [3] unused (0) -- written by tci_dram_run, 0 otherwise */
+                           adaptation (k_adapt_*), [3] FUSED's split draws: the normals and scalar draws
+                           (k_draws_rng, on a second stream one chunk ahead, overlapping the walk) --
+                           written by tci_dram_run, 0 otherwise */
   int64_t kernel_launches[4]; /* launches per class behind kernel_ms */
 } tci_dram_outputs;
 

@@ -823,13 +823,46 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
     p.chunk = chunk;
     st.draws = A.alloc<double>(n * (size_t)p.chunk * DW, &e);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dram draws)");
-    for (int64_t next = 2; next <= opt->n_steps && rc == TCI_OK;) {
+    std::vector<std::pair<int64_t, int64_t>> chunks;
+    for (int64_t next = 2; next <= opt->n_steps;) {
       int64_t end = std::min<int64_t>(opt->n_steps, next + p.chunk - 1);
       end = std::min<int64_t>(end, ((next + win - 1) / win) * win);  // chunks never cross a window
-      const int rec = end % win == 0 || end == opt->n_steps;  // the records kept in the chain kernel
-      rc = tci::dram_launch_chain(st, p, ctx->kp, ctx->rpl, next, end, rec, s, tm);
-      if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(st, p, s, tm);
+      chunks.emplace_back(next, end);
       next = end + 1;
+    }
+    // k_chain's engine splits the draws (DramParams::split; TCI_DRAWS_SPLIT=0 keeps them in one
+    // launch): chunk i + 1's normals and scalar draws go into the other of two draws buffers, drawn by
+    // extra workgroups of chunk i's k_chain launch in the CU slots its chains leave free; k_draws then
+    // only multiplies by the adapted R. The first chunk's: one k_draws_rng launch.
+    const char* split_env = getenv("TCI_DRAWS_SPLIT");
+    p.split = !p.walk && !(split_env && split_env[0] == '0') ? 1 : 0;
+    double* dbuf[2] = {st.draws, st.draws};
+    int rng_wgs = 0;
+    if (p.split && !chunks.empty()) {
+      dbuf[1] = A.alloc<double>(n * (size_t)p.chunk * DW, &e);
+      if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc(dram draws, second buffer)");
+      // the workgroup slots the chains leave (two per CU), at least a quarter of the CUs
+      const char* w_env = getenv("TCI_RNG_WGS");
+      rng_wgs = w_env && atoi(w_env) > 0 ? atoi(w_env)
+                                         : (int)std::max<int64_t>(2 * (int64_t)n_cu - n_chains, std::max(n_cu / 4, 1));
+      if ((rc = tci::dram_launch_draws_rng(st, p, chunks[0].first, chunks[0].second, 4 * std::max(n_cu, 1), s, tm)) !=
+          TCI_OK)
+        return fail(ctx, rc, "dram draws launch");
+    }
+    for (size_t i = 0; i < chunks.size() && rc == TCI_OK; ++i) {
+      const int64_t next = chunks[i].first, end = chunks[i].second;
+      const int rec = end % win == 0 || end == opt->n_steps;  // the records kept in the chain kernel
+      tci::DramState sc = st;
+      sc.draws = dbuf[i & 1];
+      // the next chunk's buffer was last read by chunk i - 1's walk, which ended before this launch
+      tci::ChainNext nx{dbuf[(i + 1) & 1], 0, -1, rng_wgs};
+      if (i + 1 < chunks.size()) {
+        nx.s_begin = chunks[i + 1].first;
+        nx.s_end = chunks[i + 1].second;
+      }
+      rc = tci::dram_launch_chain(sc, p, ctx->kp, ctx->rpl, next, end, rec, s, tm,
+                                  p.split && i + 1 < chunks.size() ? &nx : nullptr);
+      if (rc == TCI_OK && ai > 0 && end % ai == 0) rc = tci::dram_launch_adapt(sc, p, s, tm);
     }
     e = hipSuccess;
   } else {

@@ -828,10 +828,79 @@ __host__ __device__ inline bool draws_walk_wide(int64_t L) { return draws_lds_by
 // fused engine: 1 pass per k_draws workgroup (2: 80.4 vs 77.9 us per chunk, r04np); WALK: 4
 __host__ __device__ inline int draws_passes(bool walk) { return walk ? 4 : 1; }
 
+// The split draws pass (k_chain's engine, DramParams::split). The draws that do not depend on R --
+// the normals, the delayed-rejection ratio q1, the two uniforms and the unit Gamma variate -- are
+// written into the NEXT chunk's draws buffer (two buffers, alternating) by extra workgroups of the
+// k_chain launch that walks the current chunk: k_chain's 299 chain workgroups leave a CU's second
+// workgroup slot free on 213 of 256 CUs and their rounds are latency-bound. The extra workgroups
+// come after the chain workgroups in the grid (dispatched in order, so they only take slots the
+// chains left) and loop over the (chain, kRngSteps-step) units. k_draws<.., FromBuf> then only copies
+// the normals into its LDS tile and multiplies them by the chain's new R, in place. (The first chunk's
+// units: k_draws_rng, one launch before the loop.) Same normals_at / wave_q / uniform_at /
+// gamma_unit_t calls as k_draws: the same bits.
+constexpr int kRngSteps = 8;
+__host__ __device__ inline int64_t draws_rng_lds_bytes(int64_t L) { return (2 * kRngSteps * L + 8) * 8; }
+// Units first_unit, first_unit + stride, .. of chain rows s_begin..s_end into `draws` (that chunk's
+// buffer), by one kThreads workgroup; Z: 2 kRngSteps L doubles of LDS.
+__device__ __forceinline__ void draws_rng_units(const DramState& st, const DramParams& p, double* draws,
+                                                int64_t s_begin, int64_t s_end, int64_t first_unit, int64_t stride,
+                                                double* Z) {
+  constexpr int NW = kThreads / 64;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t ld = st.ld;
+  const int L = (int)ld;
+  const int64_t DW = draw_stride(ld);
+  const double inv_ds = 1.0 / p.drscale;
+  const int64_t nb = (s_end - s_begin + kRngSteps) / kRngSteps;  // units per chain
+  const int64_t nunits = st.n_chains * nb;
+  for (int64_t u = first_unit; u < nunits; u += stride) {
+    const int64_t c = u / nb;
+    const int64_t step0 = s_begin + (u - c * nb) * kRngSteps;
+    const int ns = (int)min<int64_t>(kRngSteps, s_end - step0 + 1);
+    const int P = st.npar[c];
+    const int64_t key = st.key[c];
+    double* d0 = draws + (c * p.chunk - s_begin + step0) * DW;  // row of step step0 + k: d0 + k * DW
+    draw_block_normals<kThreads>(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
+    __syncthreads();
+    for (int r = w; r < 2 * ns; r += NW) {
+      double* dz = d0 + (r >> 1) * DW + (r & 1) * ld;
+      for (int j = lane; j < P; j += 64) dz[j] = Z[r * L + j];
+    }
+    for (int k = w; k < ns; k += NW) {
+      const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
+      if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
+    }
+    if ((int)threadIdx.x < ns) {
+      const int64_t step = step0 + threadIdx.x;
+      double* sc = d0 + threadIdx.x * DW + 2 * ld;
+      sc[D_U1] = uniform_at(p.seed, key, step, P_U1);
+      sc[D_U2] = uniform_at(p.seed, key, step, P_U2);
+      sc[D_G] = p.updatesigma ? gamma_unit_t(p.seed, key, step, 0.5 * (double)st.nobs[c]) : 1.0;
+    }
+    __syncthreads();  // Z is rewritten by the next unit
+  }
+}
+__global__ __launch_bounds__(kThreads) void k_draws_rng(DramState st, DramParams p, int64_t s_begin, int64_t s_end) {
+  extern __shared__ __attribute__((aligned(16))) double dyn[];
+  draws_rng_units(st, p, st.draws, s_begin, s_end, blockIdx.x, gridDim.x, dyn);
+}
+
+// The split form's normals, already in the draws rows (k_draws_rng), into the pass's LDS tile: one
+// row per wave and loop, coalesced over j (entries past P keep the tile's zeros).
+template <int NWD>
+__device__ __forceinline__ void load_block_normals(const double* d0, int64_t DW, int64_t ld, int ns, int P, double* Z,
+                                                   int L) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  for (int r = w; r < 2 * ns; r += NWD) {
+    const double* dz = d0 + (r >> 1) * DW + (r & 1) * ld;
+    for (int j = lane; j < P; j += 64) Z[r * L + j] = dz[j];
+  }
+}
+
 // NWD waves per workgroup, CT column tiles per wave and MFMA call (launch_chain_t: 4 and 2); longer
 // rows loop over calls. The wave count and CT only move column tiles between waves and calls: same
-// bits.
-template <int NWD, int CT, int MT = kDrawMT, int WPE = kDrawsWPE>
+// bits. FromBuf: the split form (k_draws_rng above wrote the normals and scalars; z*R only).
+template <int NWD, int CT, int MT = kDrawMT, int WPE = kDrawsWPE, bool FromBuf = false>
 __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE))) void k_draws(DramState st, DramParams p, int64_t s_begin, int64_t s_end, int npass) {
   constexpr int kDrawWaves = NWD, kDrawThreads = 64 * NWD;
   constexpr int kDrawCT = CT;
@@ -857,10 +926,11 @@ __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE)))
     const int64_t step0 = s_begin + ((int64_t)blockIdx.y * npass + pass) * kDrawSteps;
     if (step0 > s_end) break;  // uniform over the workgroup
     const int ns = (int)min<int64_t>(kDrawSteps, s_end - step0 + 1);
-    if (!(TCI_DRAWS_ABLATE & 1)) draw_block_normals<kDrawThreads>(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
-    __syncthreads();
     // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
     double* d0 = drow + step0 * DW;
+    if (FromBuf) load_block_normals<kDrawWaves>(d0, DW, ld, ns, P, Z, L);
+    else if (!(TCI_DRAWS_ABLATE & 1)) draw_block_normals<kDrawThreads>(p.seed, key, step0, ns, P, p.ntry >= 2, Z, L);
+    __syncthreads();
     const auto put = [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; };
     // WALK's short pass (a 100-step chunk's last: 3 x 32 + 4 steps) runs only the row tiles it fills
     // -- an instance with fewer tiles, the same products (each depends only on its row of Z and the k
@@ -875,15 +945,16 @@ __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE)))
         else
           mfma_zr_pf<MT, kDrawCT, kDrawWaves, kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
       }
-    for (int k = w; k < ns; k += kDrawWaves) {
-      const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
-      if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
-    }
+    if (!FromBuf)
+      for (int k = w; k < ns; k += kDrawWaves) {
+        const double2 q = wave_q(Z + 2 * k * L, Z + (2 * k + 1) * L, inv_ds, P, lane);
+        if (lane == 0) d0[k * DW + 2 * ld + D_Q1] = exp(-0.5 * (q.x - q.y));  // as dr_q1
+      }
     __syncthreads();  // Z is rewritten by the next pass
   }
   // the scalar draws of the workgroup's steps, one step per thread
   const int64_t step = s_begin + (int64_t)blockIdx.y * npass * kDrawSteps + threadIdx.x;
-  if (!(TCI_DRAWS_ABLATE & 4) && threadIdx.x < npass * kDrawSteps && step <= s_end) {
+  if (!FromBuf && !(TCI_DRAWS_ABLATE & 4) && threadIdx.x < npass * kDrawSteps && step <= s_end) {
     double* sc = drow + step * DW + 2 * ld;
     sc[D_U1] = uniform_at(p.seed, key, step, P_U1);
     sc[D_U2] = uniform_at(p.seed, key, step, P_U2);
@@ -1118,7 +1189,8 @@ constexpr int kChainEPW = 1;
 
 template <int RPL, int NSEG, int EPW>
 __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, KParams kp, int64_t s_begin,
-                                                    int64_t s_end, int with_records) {
+                                                    int64_t s_end, int with_records, double* nx_draws,
+                                                    int64_t nx_begin, int64_t nx_end) {
   // Round structure (one workgroup barrier per round). At the start of a round the state after
   // row s-1 is known. The round speculates D = 2 EPW steps: proposal slot 2h + stage holds the
   // stage-1/2 proposal of step s + h, drawn around the SAME state, i.e. speculating that steps
@@ -1152,7 +1224,11 @@ __global__ __launch_bounds__(kThreads) void k_chain(DramState st, DramParams p, 
   __shared__ double xch[2][NS][4];                              // by round parity: ss, prior, in-bounds
   __shared__ double xip[2][D];                                  // by round parity: precisions of steps s + h
   const int64_t c = blockIdx.x;
-  if (c >= st.n_chains) return;
+  if (c >= st.n_chains) {  // the split draws' workgroups: the next chunk's units (nx_draws, rows nx_begin..nx_end)
+    extern __shared__ __attribute__((aligned(16))) double dyn[];
+    if (nx_draws != nullptr) draws_rng_units(st, p, nx_draws, nx_begin, nx_end, c - st.n_chains, gridDim.x - st.n_chains, dyn);
+    return;
+  }
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int lane = threadIdx.x & 63;  // re-laundered every round (launder_lane)
   const int64_t ld = st.ld;
@@ -1762,14 +1838,14 @@ __global__ __launch_bounds__(64 * kWalkWaves) __attribute__((amdgpu_waves_per_eu
 
 template <int RPL, int NSEG>
 int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, int64_t s_begin, int64_t s_end,
-                   int with_records, hipStream_t stream, LaunchTimer* timer) {
+                   int with_records, hipStream_t stream, LaunchTimer* timer, const ChainNext* nx) {
   const bool wide = p.walk != 0 && draws_walk_wide(st.ld);  // WALK: 64-row draws passes (k_draws<8, 2, 4, 2>)
   const size_t lds = (size_t)draws_lds_bytes(st.ld, wide ? kDrawMTWalk : kDrawMT);
   // 4-wave workgroups, 2 column tiles x 2 row tiles per wave and MFMA call (168 VGPRs: three
   // workgroups per CU, kDrawsWPE). Config 4 (WALK, P = 207): 72.7 ms per 1,000 steps with the 8-wave, 2-tile
   // form -> 53.6 (3 tiles: 58.0, 5: 56.4); TestData (FUSED): 105.3 -> 99.8 us per chunk against
   // 3 tiles (r03t4, r03u); the pipelined z*R loop (mfma_zr_pf) 97.6 -> 86.5 (r04g).
-  auto kd = wide ? k_draws<8, 2, kDrawMTWalk, 2> : k_draws<4, 2>;
+  auto kd = wide ? k_draws<8, 2, kDrawMTWalk, 2> : p.split ? k_draws<4, 2, kDrawMT, kDrawsWPE, true> : k_draws<4, 2>;
   const int nwd = wide ? 8 : 4;
   if (ensure_dyn_lds((const void*)kd, lds) != TCI_OK) return TCI_EHIP;
   const int npass = draws_passes(p.walk != 0);
@@ -1785,21 +1861,27 @@ int launch_chain_t(const DramState& st, const DramParams& p, const KParams& kp, 
     hipLaunchKernelGGL((k_walk<RPL, NSEG>), dim3((unsigned)((st.n_chains + kWalkWaves - 1) / kWalkWaves)),
                        dim3(64 * kWalkWaves), 0, stream, st, p,
                        kp, s_begin, s_end, with_records);
-  else
-    hipLaunchKernelGGL((k_chain<RPL, NSEG, (RPL <= 2 ? kChainEPW : 1)>), dim3((unsigned)st.n_chains), dim3(kThreads), 0,
-                       stream, st, p, kp, s_begin, s_end, with_records);
+  else {
+    auto kc = k_chain<RPL, NSEG, (RPL <= 2 ? kChainEPW : 1)>;
+    const bool rng = nx != nullptr && nx->draws != nullptr && nx->wgs > 0;
+    const size_t clds = rng ? (size_t)draws_rng_lds_bytes(st.ld) : 0;
+    if (rng && ensure_dyn_lds((const void*)kc, clds) != TCI_OK) return TCI_EHIP;
+    hipLaunchKernelGGL(kc, dim3((unsigned)(st.n_chains + (rng ? nx->wgs : 0))), dim3(kThreads), clds, stream, st, p, kp,
+                       s_begin, s_end, with_records, rng ? nx->draws : nullptr, rng ? nx->s_begin : 0,
+                       rng ? nx->s_end : -1);
+  }
   if (timer) timer->end(1, stream);
   return hipGetLastError() == hipSuccess ? TCI_OK : TCI_EHIP;
 }
 
 template <int RPL>
 int launch_chain_r(const DramState& st, const DramParams& p, const KParams& kp, int64_t a, int64_t b, int rec,
-                   hipStream_t s, LaunchTimer* timer) {
+                   hipStream_t s, LaunchTimer* timer, const ChainNext* dd) {
   switch (kp.n_seg) {
-    case 1: return launch_chain_t<RPL, 1>(st, p, kp, a, b, rec, s, timer);
-    case 2: return launch_chain_t<RPL, 2>(st, p, kp, a, b, rec, s, timer);
-    case 3: return launch_chain_t<RPL, 3>(st, p, kp, a, b, rec, s, timer);
-    case 4: return launch_chain_t<RPL, 4>(st, p, kp, a, b, rec, s, timer);
+    case 1: return launch_chain_t<RPL, 1>(st, p, kp, a, b, rec, s, timer, dd);
+    case 2: return launch_chain_t<RPL, 2>(st, p, kp, a, b, rec, s, timer, dd);
+    case 3: return launch_chain_t<RPL, 3>(st, p, kp, a, b, rec, s, timer, dd);
+    case 4: return launch_chain_t<RPL, 4>(st, p, kp, a, b, rec, s, timer, dd);
     default: return TCI_EINVAL;
   }
 }
@@ -1882,7 +1964,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(WPE))) 
   if (c >= st.n_chains || p.adaptint <= 0 || step % p.adaptint != 0) return;  // uniform exit
   const int64_t ld = st.ld;
   const int P = st.npar[c];
-  const int NT = (P + 15) >> 4, LX = 16 * NT, T = NT * (NT + 1) / 2;
+  const int NT = (P + 15) >> 4, LX = 16 * NT;
   const int shared = max(2 * kAdRB * LX, 2 * NT * 256);
   double* X = dyn;                // scatter: a batch of centred window rows [kAdRB][LX]
   double* Xw = dyn + kAdRB * LX;  //   and the same rows times their run lengths
@@ -2515,14 +2597,25 @@ int dram_launch_adapt(const DramState& st, const DramParams& p, void* stream, La
   if (timer) timer->end(2, (hipStream_t)stream);
   return rc;
 }
+int dram_launch_draws_rng(const DramState& st, const DramParams& p, int64_t s_begin, int64_t s_end, int wgs,
+                          void* stream, LaunchTimer* timer) {
+  const size_t lds = (size_t)draws_rng_lds_bytes(st.ld);
+  if (ensure_dyn_lds((const void*)k_draws_rng, lds) != TCI_OK) return TCI_EHIP;
+  if (timer) timer->begin((hipStream_t)stream);
+  hipLaunchKernelGGL(k_draws_rng, dim3((unsigned)std::max(wgs, 1)), dim3(kThreads), lds, (hipStream_t)stream, st, p, s_begin,
+                     s_end);
+  if (timer) timer->end(3, (hipStream_t)stream);
+  return finish();
+}
+int64_t dram_draws_rng_lds_bytes(int64_t ld) { return draws_rng_lds_bytes(ld); }
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,
-                      int64_t s_end, int with_records, void* stream, LaunchTimer* timer) {
+                      int64_t s_end, int with_records, void* stream, LaunchTimer* timer, const ChainNext* nx) {
   hipStream_t s = (hipStream_t)stream;
   switch (rpl) {
-    case 1: return launch_chain_r<1>(st, p, kp, s_begin, s_end, with_records, s, timer);
-    case 2: return launch_chain_r<2>(st, p, kp, s_begin, s_end, with_records, s, timer);
-    case 4: return launch_chain_r<4>(st, p, kp, s_begin, s_end, with_records, s, timer);
-    case 8: return launch_chain_r<8>(st, p, kp, s_begin, s_end, with_records, s, timer);
+    case 1: return launch_chain_r<1>(st, p, kp, s_begin, s_end, with_records, s, timer, nx);
+    case 2: return launch_chain_r<2>(st, p, kp, s_begin, s_end, with_records, s, timer, nx);
+    case 4: return launch_chain_r<4>(st, p, kp, s_begin, s_end, with_records, s, timer, nx);
+    case 8: return launch_chain_r<8>(st, p, kp, s_begin, s_end, with_records, s, timer, nx);
     default: return TCI_EINVAL;
   }
 }

@@ -14,9 +14,10 @@ namespace tci {
 // Optional device time per kernel class (tci_dram_options.kernel_times): a HIP event pair around each
 // launch of the fused / walk engines, on the launch stream, summed after the run's final
 // synchronisation. Classes: 0 the draws pass (k_draws), 1 the chain walk (k_chain / k_walk), 2 the
-// covariance adaptation (k_adapt_*).
+// covariance adaptation (k_adapt_*), 3 the split draws' first chunk (k_draws_rng; the later chunks'
+// are drawn inside the k_chain launches, class 1).
 struct LaunchTimer {
-  static constexpr int kClasses = 3;
+  static constexpr int kClasses = 4;
   struct Mark {
     int cls;
     hipEvent_t a, b;
@@ -158,6 +159,8 @@ struct DramParams {
   int64_t walk;        // fused engine: 1 = one wavefront per chain walks the chunk (k_walk), 0 = k_chain
   int64_t win;         // window rows per chain: adaptint, or (no adaptation) 100; the
                        // records are merged window by window (k_stats), the same partition for every engine
+  int64_t split;       // k_chain's engine: the draws split in two (the state-independent ones drawn one chunk
+                       // ahead by extra k_chain workgroups; k_draws multiplies by R only). Same bits.
 };
 
 int dram_launch_init(const DramState& st, const double* qcov_diag, const double* sigma2_0, void* stream);
@@ -170,9 +173,23 @@ int dram_launch_step_incr(const DramState& st, void* stream);
 int dram_launch_init_stats(const DramState& st, const DramParams& p, void* stream);
 // Fused engine: chain rows s_begin..s_end (each chain's ssfun inside the kernel); leaves *st.step = s_end.
 // with_records: s_end ends a window (or the run) -- the window's records are kept by the same kernel.
+// The split draws (DramParams::split): k_chain's launch also draws the next chunk's normals and scalar
+// draws (rows s_begin..s_end) into that chunk's buffer with `wgs` extra workgroups.
+struct ChainNext {
+  double* draws;
+  int64_t s_begin, s_end;
+  int wgs;
+};
 int dram_launch_chain(const DramState& st, const DramParams& p, const KParams& kp, int rpl, int64_t s_begin,
-                      int64_t s_end, int with_records, void* stream, LaunchTimer* timer = nullptr);
-int64_t dram_chain_lds_bytes(int64_t ld, int rpl);  // LDS per workgroup of the fused engine
+                      int64_t s_end, int with_records, void* stream, LaunchTimer* timer = nullptr,
+                      const ChainNext* next = nullptr);
+int64_t dram_chain_lds_bytes(int64_t ld, int rpl);
+// Split draws (DramParams::split): the normals, q1 and scalar draws of chain rows s_begin..s_end into
+// st.draws (that chunk's buffer) by `wgs` workgroups -- the first chunk's; k_chain draws the later ones
+// (ChainNext). Timer class 3.
+int dram_launch_draws_rng(const DramState& st, const DramParams& p, int64_t s_begin, int64_t s_end, int wgs,
+                          void* stream, LaunchTimer* timer = nullptr);
+int64_t dram_draws_rng_lds_bytes(int64_t ld);  // LDS per workgroup of the fused engine
 // LDS of the adaptation kernel dram_launch_adapt picks for (pmax, adaptint), dynamic plus the kernel's
 // static __shared__: the window's run table grows with adaptint (4 bytes per row), so tci_dram_run
 // refuses an adaptint past the CU's LDS before any launch.

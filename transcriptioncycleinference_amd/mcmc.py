@@ -86,7 +86,8 @@ class DramResult:
     s2chain: Optional[np.ndarray]
     elapsed_ms: float
     qcov_R: Optional[np.ndarray] = None   # final proposal factor (upper, R'R = mcmcstat results.qcov)
-    kernel_ms: Optional[np.ndarray] = None        # DramOptions.kernel_times: ms per class (draws, walk, adapt, -)
+    kernel_ms: Optional[np.ndarray] = None        # DramOptions.kernel_times: ms per class (draws, walk, adapt,
+    #                                               the split draws' first-chunk launch; include/tci.h)
     kernel_launches: Optional[np.ndarray] = None  # and launches per class
 
 
