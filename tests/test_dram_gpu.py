@@ -319,6 +319,27 @@ def test_chunk_size_does_not_change_the_chains(lk, engine):
         np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
 
 
+@pytest.mark.parametrize("ntry,updatesigma,max_chunk", [(2, True, 0), (1, True, 23), (2, False, 9)])
+def test_split_draws_equal_the_one_launch_draws(lk, monkeypatch, ntry, updatesigma, max_chunk):
+    """The fused engine's split draws (the next chunk's normals and scalar draws by extra k_chain
+    workgroups into the other draws buffer, k_draws multiplying by R in place) against
+    the one-launch draws pass (TCI_DRAWS_SPLIT=0): every output bitwise equal -- stage-2 normals
+    zeroed (ntry = 1), no Gamma draws (updatesigma off), chunks shorter than a window and a short
+    last chunk."""
+    from transcriptioncycleinference_amd.mcmc import DramOptions
+
+    ids = list(range(1, 299, 13))
+    o = DramOptions(n_steps=377, burnintime=150, adaptint=100, stats_from=120, thin=4, seed=23, ntry=ntry,
+                    updatesigma=updatesigma, engine="fused", max_chunk=max_chunk)
+    monkeypatch.setenv("TCI_DRAWS_SPLIT", "1")
+    a, _ = run(lk, ids, o)
+    monkeypatch.setenv("TCI_DRAWS_SPLIT", "0")
+    b, _ = run(lk, ids, o)
+    for f in ("chain", "s2chain", "mean", "std", "final_theta", "sigma_mean", "sigma_std", "accept_rate", "n_evals"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    assert np.median(a.accept_rate) > 0.01
+
+
 @pytest.mark.parametrize("engine", ["fused", "batched"])
 def test_adapted_proposal_is_the_scaled_chain_covariance(lk, engine):
     """mcmcstat's adaptation: after the last adaptation row n (n >= burnintime), the proposal

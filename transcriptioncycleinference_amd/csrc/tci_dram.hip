@@ -906,7 +906,7 @@ __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE)))
   constexpr int kDrawCT = CT;
   constexpr int kDrawSteps = 8 * MT;  // steps per pass
   extern __shared__ __attribute__((aligned(16))) double dyn[];
-  const int64_t c = blockIdx.x;
+  const int64_t c = blockIdx.x, by = blockIdx.y;
   if (c >= st.n_chains) return;
   const int64_t ld = st.ld;
   const int L = (int)ld;
@@ -923,7 +923,7 @@ __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE)))
   const double inv_ds = 1.0 / p.drscale;
   double* drow = st.draws + (c * p.chunk - s_begin) * DW;  // row of step s: drow + s * DW
   for (int pass = 0; pass < npass; ++pass) {
-    const int64_t step0 = s_begin + ((int64_t)blockIdx.y * npass + pass) * kDrawSteps;
+    const int64_t step0 = s_begin + (by * npass + pass) * kDrawSteps;
     if (step0 > s_end) break;  // uniform over the workgroup
     const int ns = (int)min<int64_t>(kDrawSteps, s_end - step0 + 1);
     // z*R straight to the draws rows: row r of Z is step step0 + r/2, stage r&1
@@ -934,11 +934,13 @@ __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE)))
     const auto put = [=](int r, int j, double v) { d0[(r >> 1) * DW + (r & 1) * ld + j] = v; };
     // WALK's short pass (a 100-step chunk's last: 3 x 32 + 4 steps) runs only the row tiles it fills
     // -- an instance with fewer tiles, the same products (each depends only on its row of Z and the k
-    // order): config 4 2,381 -> 2,289 us per launch (r05p); the fused engine's 128-VGPR instance
-    // spilled more with it (77.4 -> 78.1 us per TestData chunk) and keeps one instance
+    // order): config 4 2,381 -> 2,289 us per launch (r05p); the fused engine's one-launch instance
+    // spilled more with it (77.4 -> 78.1 us per TestData chunk) and keeps one instance; its split
+    // (FromBuf, 117 VGPRs) form has the room: 54.6 -> 53.5 us per chunk (r06t1; XCD-grouped chain
+    // blocks, cdna_hip_programming.md T1, measured slower: 54.9 -> 60.5, r06t2)
     if (!(TCI_DRAWS_ABLATE & 2))
       for (int top = ((P + 15) >> 4) - 1; top >= 0; top -= kDrawWaves * kDrawCT) {
-        if (MT > 2 && 2 * ns <= 16)
+        if ((MT > 2 || FromBuf) && 2 * ns <= 16)
           mfma_zr_pf<1, kDrawCT, kDrawWaves, kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
         else if (MT > 2 && 2 * ns <= 32)
           mfma_zr_pf<(MT > 2 ? 2 : MT), kDrawCT, kDrawWaves, kDrawsPF>(Z, L, 2 * ns, Rg, P, top, put);
@@ -953,7 +955,7 @@ __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE)))
     __syncthreads();  // Z is rewritten by the next pass
   }
   // the scalar draws of the workgroup's steps, one step per thread
-  const int64_t step = s_begin + (int64_t)blockIdx.y * npass * kDrawSteps + threadIdx.x;
+  const int64_t step = s_begin + by * npass * kDrawSteps + threadIdx.x;
   if (!FromBuf && !(TCI_DRAWS_ABLATE & 4) && threadIdx.x < npass * kDrawSteps && step <= s_end) {
     double* sc = drow + step * DW + 2 * ld;
     sc[D_U1] = uniform_at(p.seed, key, step, P_U1);
