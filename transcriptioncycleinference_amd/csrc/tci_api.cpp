@@ -834,8 +834,10 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
     // launch): chunk i + 1's normals and scalar draws go into the other of two draws buffers, drawn by
     // extra workgroups of chunk i's k_chain launch in the CU slots its chains leave free; k_draws then
     // only multiplies by the adapted R. The first chunk's: one k_draws_rng launch.
+    // Only while the chains leave slots free (at most two chain workgroups per CU, AUTO's FUSED range):
+    // past that the extra workgroups would wait behind the chains.
     const char* split_env = getenv("TCI_DRAWS_SPLIT");
-    p.split = !p.walk && !(split_env && split_env[0] == '0') ? 1 : 0;
+    p.split = !p.walk && n_chains < 2 * (int64_t)std::max(n_cu, 1) && !(split_env && split_env[0] == '0') ? 1 : 0;
     double* dbuf[2] = {st.draws, st.draws};
     int rng_wgs = 0;
     if (p.split && !chunks.empty()) {
@@ -844,7 +846,7 @@ int tci_dram_run(tci_ctx* ctx, const tci_dram_options* opt, int64_t n_chains, co
       // the workgroup slots the chains leave (two per CU), at least a quarter of the CUs
       const char* w_env = getenv("TCI_RNG_WGS");
       rng_wgs = w_env && atoi(w_env) > 0 ? atoi(w_env)
-                                         : (int)std::max<int64_t>(2 * (int64_t)n_cu - n_chains, std::max(n_cu / 4, 1));
+                                         : (int)std::max<int64_t>(2 * (int64_t)n_cu - n_chains, n_cu / 4);
       if ((rc = tci::dram_launch_draws_rng(st, p, chunks[0].first, chunks[0].second, 4 * std::max(n_cu, 1), s, tm)) !=
           TCI_OK)
         return fail(ctx, rc, "dram draws launch");
