@@ -5,7 +5,9 @@ in-bounds rows, TCI_LK_COMPACT=1) and without it (one-wave blocks over every row
 each wave, TCI_LK_COMPACT=0). Both contexts hold the same cells; the SS of every batch must be equal
 bit for bit. Prints per-launch µs (HIP events around 40 back-to-back launches, both kernels of the
 listed form included) over interleaved rounds, and the evals/s each gives.
-usage: python scripts/lk_compact_ab.py [rounds]"""
+usage: python scripts/lk_compact_ab.py [rounds]
+Needs the row-list build (TCI_LK_COMPACT): the commit before "Remove the row-list likelihood form";
+the shipped library ignores the switch (measured, not kept)."""
 import json
 import os
 import sys
