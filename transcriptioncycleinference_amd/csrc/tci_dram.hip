@@ -416,7 +416,7 @@ __device__ __forceinline__ void mfma_zr(const double* Z, int zs, int M, const do
 template <int MT, int CT, int NWV, int PF, class Store>
 __device__ __forceinline__ void mfma_zr_pf(const double* Z, int zs, int M, const double* __restrict__ Rg, int P,
                                            int top, Store store) {
-  static_assert(PF >= 1 && PF <= 2, "reads reach k = P + 4 PF - 2: draws_lds_bytes pads 8 doubles");
+  static_assert(PF >= 1 && PF <= 4, "reads reach k = P + 4 PF - 2: draws_lds_bytes pads 16 doubles");
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int row = lane & 15, kq = lane >> 4;
   int nt[CT], kmx[CT], jv[CT], jc[CT];
@@ -806,7 +806,10 @@ __device__ __forceinline__ void draw_block_normals(uint64_t seed, int64_t c, int
 constexpr int kDrawsWPE = 3;             // waves per SIMD k_draws is compiled for (<= 168 VGPRs): at 4
                                           // (128 VGPRs) it spilled 34 VGPRs, 76.9 -> 75.5 us per TestData
                                           // chunk at 3 (r05dw; three 37 KB workgroups per CU)
-constexpr int kDrawsPF = 2;               // R values prefetched this many k-steps ahead (mfma_zr PF)
+constexpr int kDrawsPF = 4;               // R values prefetched this many k-steps ahead (mfma_zr PF): 4 against
+                                          // 2, per launch, split z*R (TestData) 53.3 -> 51.3 us, WALK (config
+                                          // 4) 4,300 -> 4,119 us (r06pfd, r06pfc4); the extra k-steps of a
+                                          // whole ring multiply zero R entries (the same bits)
 constexpr int kDrawMT = 2;                // MFMA row tiles per pass (16 rows each), 4-wave workgroups
 enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a draws row
 
@@ -815,7 +818,7 @@ enum DrawSlot { D_Q1 = 0, D_U1 = 1, D_U2 = 2, D_G = 3 };  // scalar slots of a d
 // normals (74 KB at P = 136) left one workgroup per CU, and that layout took 144 us per TestData
 // chunk against 105 us with R from L2 and four 35 KB workgroups per CU (r03n/r03o).
 // (+ 8 doubles: mfma_zr_pf's reads past the last row's P entries, zeroed with the pads)
-__host__ __device__ inline int64_t draws_lds_bytes(int64_t L, int mt = kDrawMT) { return (2 * 8 * mt * L + 8) * 8; }
+__host__ __device__ inline int64_t draws_lds_bytes(int64_t L, int mt = kDrawMT) { return (2 * 8 * mt * L + 16) * 8; }
 // WALK (thousands of chains): their R triangles (171 KB per chain at P = 207, 1.7 GB for config
 // 4) stream from HBM, once per pass, so the passes there are twice as long -- 4 row tiles (64 rows)
 // in an 8-wave workgroup of 256-VGPR waves, one per CU (106 KB of normals): the R traffic per row
@@ -839,7 +842,7 @@ __host__ __device__ inline int draws_passes(bool walk) { return walk ? 4 : 1; }
 // units: k_draws_rng, one launch before the loop.) Same normals_at / wave_q / uniform_at /
 // gamma_unit_t calls as k_draws: the same bits.
 constexpr int kRngSteps = 8;
-__host__ __device__ inline int64_t draws_rng_lds_bytes(int64_t L) { return (2 * kRngSteps * L + 8) * 8; }
+__host__ __device__ inline int64_t draws_rng_lds_bytes(int64_t L) { return (2 * kRngSteps * L + 16) * 8; }
 // Units first_unit, first_unit + stride, .. of chain rows s_begin..s_end into `draws` (that chunk's
 // buffer), by one kThreads workgroup; Z: 2 kRngSteps L doubles of LDS.
 __device__ __forceinline__ void draws_rng_units(const DramState& st, const DramParams& p, double* draws,
@@ -916,7 +919,7 @@ __global__ __launch_bounds__(64 * NWD) __attribute__((amdgpu_waves_per_eu(WPE)))
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   double* Z = dyn;
   // finite LDS under every z*R read (mfma_zr_pf): the pads past P and past the last row stay zero
-  for (int e = threadIdx.x; e < 2 * kDrawSteps * L + 8; e += kDrawThreads) Z[e] = 0.0;
+  for (int e = threadIdx.x; e < 2 * kDrawSteps * L + 16; e += kDrawThreads) Z[e] = 0.0;
   __syncthreads();
   const double* Rg = st.Rd + c * tri_stride(ld);
   const double a = 0.5 * (double)st.nobs[c];
